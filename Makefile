@@ -1,0 +1,59 @@
+# Builds libmchecksum.so (the drop-in mchecksum C ABI + MI355X batch kernels),
+# libmchecksum_bench.so (device-side synthetic data for tests/bench) and the
+# CPU oracle (test infrastructure, oracle/_build).  gfx950 only.
+HIPCC     ?= /opt/rocm/bin/hipcc
+CC        ?= gcc
+ARCH      ?= gfx950
+BUILD     := build
+LIBDIR    := mercury_amd/lib
+CSRC      := mercury_amd/csrc
+INC       := -Iinclude -I$(CSRC)
+CFLAGS    ?= -O2 -g -std=c11 -Wall -Wextra -fPIC -fvisibility=hidden
+HIPFLAGS  ?= -O3 -g --offload-arch=$(ARCH) -fPIC -fvisibility=hidden -std=c++17 -Wall \
+             -munsafe-fp-atomics
+EXTRA_HIPFLAGS ?=
+
+LIB       := $(LIBDIR)/libmchecksum.so
+BENCHLIB  := $(LIBDIR)/libmchecksum_bench.so
+COBJS     := $(BUILD)/mchecksum_cpu.o $(BUILD)/mchecksum_models.o $(BUILD)/crc_tables.o
+GOBJS     := $(BUILD)/mchecksum_gpu.o
+
+all: $(LIB) $(BENCHLIB) oracle
+
+$(BUILD) $(LIBDIR):
+	mkdir -p $@
+
+$(BUILD)/%.o: $(CSRC)/%.c $(wildcard $(CSRC)/*.h) include/mchecksum.h | $(BUILD)
+	$(CC) $(CFLAGS) $(INC) -c $< -o $@
+
+$(BUILD)/mchecksum_gpu.o: $(CSRC)/mchecksum_gpu.hip $(wildcard $(CSRC)/*.h) include/mchecksum_gpu.h | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) $(EXTRA_HIPFLAGS) $(INC) -c $< -o $@
+
+$(BUILD)/bench_datagen.o: $(CSRC)/bench_datagen.hip | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) $(INC) -c $< -o $@
+
+$(LIB): $(COBJS) $(GOBJS) | $(LIBDIR)
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^ -lpthread -Wl,-soname,libmchecksum.so.2
+
+$(BENCHLIB): $(BUILD)/bench_datagen.o | $(LIBDIR)
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^
+
+oracle:
+	$(MAKE) -C oracle
+
+# CPU-only artefacts (no hipcc needed): streaming API for host tests.
+cpu: $(LIBDIR)/libmchecksum_cpu.so
+$(LIBDIR)/libmchecksum_cpu.so: $(COBJS) | $(LIBDIR)
+	$(CC) -shared -o $@ $^ -lpthread
+
+# Disassembly for roofline/occupancy inspection.
+asm: | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) $(EXTRA_HIPFLAGS) $(INC) --save-temps -c $(CSRC)/mchecksum_gpu.hip -o $(BUILD)/asm_tmp.o \
+	  -Rpass-analysis=kernel-resource-usage 2> $(BUILD)/resource_usage.txt; \
+	mv mchecksum_gpu-hip-amdgcn-amd-amdhsa-$(ARCH).s $(BUILD)/ 2>/dev/null; rm -f mchecksum_gpu-hip-*; true
+
+clean:
+	rm -rf $(BUILD) $(LIBDIR)/*.so
+	$(MAKE) -C oracle clean
+
+.PHONY: all oracle clean cpu asm

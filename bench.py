@@ -1,0 +1,218 @@
+#!/usr/bin/env python3
+"""bench.py -- headline benchmark of the MI355X mchecksum batch path.
+
+Metric (BASELINE.json): GiB/s checksummed (device-resident), CRC32c,
+64K x 64 KiB payloads.  One "step" = one batch launch over the whole
+per-GPU batch (65536 payloads of 64 KiB = 4 GiB), inputs already in HBM.
+
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
+each rank owns a contiguous shard of a global batch (weak scaling: per-GPU
+work fixed), generated on its own device; no collective in the timed region.
+After timing, RCCL all_gather of the per-shard CRC arrays to check the
+gathered result and an all_reduce(MAX) of the timings.
+
+Prints ONE JSON line on rank 0 (contract in the task statement), with
+`roofline` (HIP-event kernel time vs HBM peak) and `cpu_baseline` (oracle on
+this host's cores, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md:36
+
+CONFIGS = {
+    # name: (method, count, length, seed, layout)
+    "metric": ("crc32c", 65536, 65536, 0x4D43310000000005, "fixed"),
+    "c2": ("crc32c", 65536, 4096, 0x4D43310000000002, "fixed"),
+    "c3": ("crc64", 8192, 1 << 20, 0x4D43310000000003, "fixed"),
+    "c4": ("crc32c", 262144, None, 0x4D43310000000004, "offsets"),
+}
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--config", default="metric", choices=sorted(CONFIGS))
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=1.5, help="wall budget of the CPU baseline sample")
+    p.add_argument("--parity-samples", type=int, default=64)
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    from mercury_amd import gpu as G
+
+    method, count, length, seed, layout = CONFIGS[args.config]
+    stream = torch.cuda.current_stream()
+    G.prepare(method)
+
+    # ---- per-rank shard of a global batch, generated on the device -------
+    if layout == "fixed":
+        nbytes = count * length
+        data = torch.empty(nbytes + 64, dtype=torch.uint8, device=dev)
+        first_word = (rank * nbytes) // 8  # shard r = payloads [r*count, (r+1)*count)
+        G.fill_splitmix(data, seed, first_word=first_word)
+        offsets_dev = offsets_host = None
+        payload_bytes = nbytes
+        run = lambda out: G.checksum_fixed(method, data, length, count=count, out=out)  # noqa: E731
+    else:
+        from oracle import oracle as O  # layout table only (host offsets), not a checksum
+        offsets_host = O.varlen_offsets(seed ^ rank, count)
+        payload_bytes = int(offsets_host[-1])
+        data = torch.empty(payload_bytes + 64, dtype=torch.uint8, device=dev)
+        G.fill_splitmix(data, seed ^ rank)
+        offsets_dev = torch.from_numpy(offsets_host.astype(np.int64)).to(dev)
+        G.checksum_offsets(method, data, offsets_dev, offsets_host=offsets_host)  # validates the table once
+        run = lambda out: G.checksum_offsets(method, data, offsets_dev, out=out)  # noqa: E731
+    out = torch.empty(count, dtype=G.out_dtype(method), device=dev)
+    torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        run(out)
+    torch.cuda.synchronize()
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        run(out)
+        ev[i][1].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+    t = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall_max, kern_ms_max = float(t[0]), float(t[1])
+
+    # ---- parity on the gathered result (outside the timed region) --------
+    crcs = out
+    if world > 1:
+        gathered = [torch.empty_like(out) for _ in range(world)]
+        dist.all_gather(gathered, out)
+        crcs = torch.cat(gathered)
+    parity = "unchecked"
+    if rank == 0:
+        from oracle import oracle as O
+        got = G.as_unsigned(crcs)
+        rng = np.random.default_rng(1234)
+        n_tot = count * world
+        idx = np.unique(np.concatenate([[0, n_tot - 1], rng.integers(0, n_tot, args.parity_samples)]))
+        bad = 0
+        for gi in idx:
+            r, i = divmod(int(gi), count)
+            if layout == "fixed":
+                want = O.splitmix_batch_fixed(method, seed, length, length, int(gi), 1)[0]
+            else:
+                if r != 0:
+                    continue  # other ranks' varlen shards use their own seed; rank 0 checks its own
+                lo, hi = int(offsets_host[i]), int(offsets_host[i + 1])
+                want = O.crc(method, data[lo:hi].cpu().numpy())
+            bad += int(got[gi] != want)
+        parity = f"bit-exact ({len(idx)} sampled payloads vs oracle)" if bad == 0 else f"MISMATCH {bad}/{len(idx)}"
+
+    total_bytes = payload_bytes * world
+    gib_s = total_bytes / wall_max / 2**30
+    out_bytes = count * (4 if G.out_dtype(method) == torch.int32 else 8)
+    alg_bytes = payload_bytes + out_bytes + (8 * (count + 1) if layout == "offsets" else 0)
+    achieved = alg_bytes / (kern_ms_max * 1e-3) / 1e9
+
+    result = None
+    if rank == 0:
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", f"pmc_traffic_{args.config}.json")
+        if os.path.exists(pmc):
+            try:
+                traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        result = {
+            "metric": "GiB/s checksummed (device-resident), CRC32c, 64K x 64 KiB payloads"
+            if args.config == "metric" else f"GiB/s checksummed (device-resident), {args.config}",
+            "value": round(gib_s, 2),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(wall_max / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (splitmix64 bytes generated on device)",
+            "config": {"workload": f"{method} over {count} x {length if length else 'U[64B,64KiB]'} B payloads per GPU"
+                       + (" (offsets table)" if layout == "offsets" else ""),
+                       "method": method, "payloads_per_gpu": count, "payload_bytes": length,
+                       "bytes_per_gpu": payload_bytes, "lanes_per_payload": G.lanes_per_payload(method, length or 65536)
+                       if layout == "fixed" else 64, "parallelism": f"shard{world}"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel_ms": round(kern_ms_max, 4), "algorithmic_bytes_per_launch": alg_bytes},
+            "parity": parity,
+        }
+        if world == 1 and not args.no_cpu_baseline and layout == "fixed":
+            result["cpu_baseline"] = cpu_baseline(method, seed, length, args.cpu_seconds)
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return result
+
+
+def cpu_baseline(method, seed, length, budget_s):
+    """Oracle (CPU restatement of mchecksum) on this host's cores over a bounded
+    sample of the same workload: the reference's own mchecksum is absent from
+    the reference tree, so kind = "port"."""
+    from oracle import oracle as O
+    threads = max(1, min(16, os.cpu_count() or 1))
+    n = 4096 if length <= 65536 else 256
+    host = O.splitmix_bytes(n * length, seed)
+    variant = "sse42" if method == "crc32c" else "table"
+    O.batch_fixed(method, host, length, length, 64, variant=variant, nthreads=threads)  # warm
+    passes, t0 = 0, time.perf_counter()
+    while True:
+        O.batch_fixed(method, host, length, length, n, variant=variant, nthreads=threads)
+        passes += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s and passes >= 2:
+            break
+    val = passes * n * length / el / 2**30
+    return {"value": round(val, 2), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "variant": "x86 SSE4.2 crc32 instruction" if variant == "sse42" else "slicing table",
+            "sample": f"{passes} passes over {n} x {length} B of the same splitmix payloads ({el:.2f} s wall)"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,95 @@
+/*
+ * mchecksum_gpu.h -- MI355X batch entry points of libmchecksum.
+ *
+ * These are ADDITIONAL extern "C" entry points next to the unchanged
+ * mchecksum streaming API (<mchecksum.h>).  Where Mercury streams the bytes
+ * of one serialized proc buffer through mchecksum_update/get
+ * (src/mercury_proc.c:387-406, 358-384), a batch entry point computes the
+ * same value for many independent, device-resident payloads at once:
+ *
+ *   value[i] == mchecksum_get() after mchecksum_update(payload_i, len_i)
+ *
+ * bit for bit, for every method the GPU supports (crc32c, crc64).  The
+ * whole-buffer form is exact because, in Mercury's default non-XDR build, the
+ * proc checksum is the CRC of the contiguous serialized bytes
+ * buf[0 : hg_proc_get_size_used) (src/mercury_proc.h:124-143,162-181;
+ * SURVEY.md 0.4).
+ *
+ * Memory: dev_base, dev_offsets and dev_out are device pointers (hipMalloc or
+ * any device-accessible allocation).  Payload bytes are read in aligned
+ * 16-byte granules, so the allocation must be readable up to the next 16-byte
+ * boundary after the last payload byte (hipMalloc allocations always are).
+ * dev_out receives `count` host-order integers of the method's size
+ * (uint32_t for crc32c, uint64_t for crc64).
+ *
+ * Streams: `stream` is a hipStream_t (NULL = the default stream).  Calls are
+ * asynchronous and capture-safe once mchecksum_gpu_prepare() has run for the
+ * method on the current device (it uploads the lookup tables).
+ *
+ * There is NO host fallback: without a usable HIP device every call returns
+ * MCHECKSUM_GPU_ENODEV.
+ */
+#ifndef MCHECKSUM_GPU_H
+#define MCHECKSUM_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "mchecksum.h"
+
+#define MCHECKSUM_GPU_OK        0
+#define MCHECKSUM_GPU_EINVAL    (-1) /* bad argument */
+#define MCHECKSUM_GPU_ENODEV    (-2) /* no usable HIP device */
+#define MCHECKSUM_GPU_EMETHOD   (-3) /* method not supported on GPU */
+#define MCHECKSUM_GPU_EHIP      (-4) /* HIP runtime error (see error string) */
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* 1 if a HIP device is usable by this process, else 0. */
+MCHECKSUM_PUBLIC int
+mchecksum_gpu_available(void);
+
+/* Build and upload the lookup tables for hash_method on the current device.
+ * Optional (done lazily on first use); call it before hipGraph capture. */
+MCHECKSUM_PUBLIC int
+mchecksum_gpu_prepare(const char *hash_method);
+
+/* Fixed-size batch: payload i = dev_base[i*stride, i*stride + len), i < count. */
+MCHECKSUM_PUBLIC int
+mchecksum_gpu_checksum_fixed(const char *hash_method, const void *dev_base,
+    size_t stride, size_t len, size_t count, void *dev_out, void *stream);
+
+/* Variable-size batch: payload i = dev_base[dev_offsets[i], dev_offsets[i+1]),
+ * i < count; dev_offsets holds count + 1 non-decreasing byte offsets
+ * (the C4 "offsets table" layout; payloads may start at any byte). */
+MCHECKSUM_PUBLIC int
+mchecksum_gpu_checksum_offsets(const char *hash_method, const void *dev_base,
+    const uint64_t *dev_offsets, size_t count, void *dev_out, void *stream);
+
+/* Batched verify of received payloads against expected values (e.g. the
+ * payload hash carried in the 4-byte HG header, src/mercury_header.c:111-112,
+ * after ntohl): dev_status[i] = 1 if CRC(payload i) != dev_expected[i] else 0,
+ * and *dev_mismatches (device uint32) is incremented by the number of
+ * mismatches (caller zeroes it).  dev_expected holds host-order values of the
+ * method's size.  Either status pointer may be NULL. */
+MCHECKSUM_PUBLIC int
+mchecksum_gpu_verify_offsets(const char *hash_method, const void *dev_base,
+    const uint64_t *dev_offsets, size_t count, const void *dev_expected,
+    uint8_t *dev_status, uint32_t *dev_mismatches, void *stream);
+
+/* Lanes cooperating on one payload that checksum_fixed would choose for
+ * this length (1..64), for reporting; -1 on error. */
+MCHECKSUM_PUBLIC int
+mchecksum_gpu_lanes_per_payload(const char *hash_method, size_t len);
+
+/* Human-readable text for the last error on this thread. */
+MCHECKSUM_PUBLIC const char *
+mchecksum_gpu_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MCHECKSUM_GPU_H */

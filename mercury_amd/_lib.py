@@ -1,0 +1,81 @@
+"""Loads libmchecksum.so -- the drop-in mchecksum C ABI plus the MI355X batch
+entry points (include/mchecksum.h, include/mchecksum_gpu.h).
+
+There is no Python or CPU fallback for the batch path: if the shared library
+is missing the import fails loudly; if no HIP device is usable, every batch
+call raises (MCHECKSUM_GPU_ENODEV).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_DIR = os.path.join(_HERE, "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libmchecksum.so")
+BENCH_LIB_PATH = os.path.join(LIB_DIR, "libmchecksum_bench.so")
+
+# Every function the public headers declare (checked against include/*.h by
+# tests/test_capi.py).
+STREAMING_SYMBOLS = ("mchecksum_init", "mchecksum_destroy", "mchecksum_reset", "mchecksum_get_size",
+                     "mchecksum_get", "mchecksum_update")
+GPU_SYMBOLS = ("mchecksum_gpu_available", "mchecksum_gpu_prepare", "mchecksum_gpu_checksum_fixed",
+               "mchecksum_gpu_checksum_offsets", "mchecksum_gpu_verify_offsets",
+               "mchecksum_gpu_lanes_per_payload", "mchecksum_gpu_last_error")
+
+_lib = None
+_bench = None
+
+c_void_p, c_size_t, c_int, c_char_p = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_char_p
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise ImportError(f"{path} is missing: build it with `make` (or __graft_entry__.build()); "
+                          "mercury_amd has no fallback implementation")
+    L = ctypes.CDLL(path)
+    L.mchecksum_init.argtypes = [c_char_p, ctypes.POINTER(c_void_p)]
+    L.mchecksum_init.restype = c_int
+    L.mchecksum_destroy.argtypes = [c_void_p]
+    L.mchecksum_destroy.restype = c_int
+    L.mchecksum_reset.argtypes = [c_void_p]
+    L.mchecksum_reset.restype = c_int
+    L.mchecksum_get_size.argtypes = [c_void_p]
+    L.mchecksum_get_size.restype = c_size_t
+    L.mchecksum_get.argtypes = [c_void_p, c_void_p, c_size_t, c_int]
+    L.mchecksum_get.restype = c_int
+    L.mchecksum_update.argtypes = [c_void_p, c_void_p, c_size_t]
+    L.mchecksum_update.restype = c_int
+    L.mchecksum_gpu_available.argtypes = []
+    L.mchecksum_gpu_available.restype = c_int
+    L.mchecksum_gpu_prepare.argtypes = [c_char_p]
+    L.mchecksum_gpu_prepare.restype = c_int
+    L.mchecksum_gpu_checksum_fixed.argtypes = [c_char_p, c_void_p, c_size_t, c_size_t, c_size_t, c_void_p, c_void_p]
+    L.mchecksum_gpu_checksum_fixed.restype = c_int
+    L.mchecksum_gpu_checksum_offsets.argtypes = [c_char_p, c_void_p, c_void_p, c_size_t, c_void_p, c_void_p]
+    L.mchecksum_gpu_checksum_offsets.restype = c_int
+    L.mchecksum_gpu_verify_offsets.argtypes = [c_char_p, c_void_p, c_void_p, c_size_t, c_void_p, c_void_p,
+                                               c_void_p, c_void_p]
+    L.mchecksum_gpu_verify_offsets.restype = c_int
+    L.mchecksum_gpu_lanes_per_payload.argtypes = [c_char_p, c_size_t]
+    L.mchecksum_gpu_lanes_per_payload.restype = c_int
+    L.mchecksum_gpu_last_error.argtypes = []
+    L.mchecksum_gpu_last_error.restype = c_char_p
+    _lib = L
+    return L
+
+
+def load_bench_library(path: str = BENCH_LIB_PATH) -> ctypes.CDLL:
+    global _bench
+    if _bench is not None:
+        return _bench
+    if not os.path.exists(path):
+        raise ImportError(f"{path} is missing: build it with `make`")
+    B = ctypes.CDLL(path)
+    B.mck_bench_fill_splitmix.argtypes = [c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, c_void_p]
+    B.mck_bench_fill_splitmix.restype = c_int
+    _bench = B
+    return B

@@ -1,0 +1,330 @@
+/*
+ * mchecksum_cpu.c -- the streaming mchecksum API (init/reset/update/get/
+ * get_size/destroy) that Mercury calls per serialized field.
+ *
+ * Callers and what they need:
+ *   hg_proc_create   src/mercury_proc.c:52-78   init("crc32c"...), get_size
+ *   hg_proc_reset    src/mercury_proc.c:203-211 reset
+ *   HG_PROC_TYPE/BYTES -> hg_proc_checksum_update  src/mercury_proc.c:387-406
+ *                    update(field bytes) -- 1..8 bytes per field, or one
+ *                    large update for raw byte arrays
+ *   hg_proc_flush    src/mercury_proc.c:358-384 get(..., MCHECKSUM_FINALIZE)
+ *   hg_core_header_{request,response}_proc  src/mercury_core_header.c:175-289
+ *                    crc16 over host-order header field values
+ * Callers pass HOST pointers to tiny fields, so this surface stays on the
+ * CPU by design; batches of device-resident payloads use <mchecksum_gpu.h>.
+ *
+ * Implementation: reflected models run slicing-by-8 on the reflected
+ * register (tables built once per model under pthread_once), crc32c uses the
+ * SSE4.2 crc32 instruction when the CPU has it; MSB-first models run a byte
+ * table.  No global mutable state after table construction, so distinct
+ * objects are safe to use from different threads concurrently.
+ */
+#define _GNU_SOURCE
+#include "mchecksum.h"
+#include "mchecksum_models.h"
+
+#include <pthread.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+struct mchecksum_object {
+    const mck_model_t *m;
+    const uint64_t (*t)[256]; /* slicing tables (reflected) or t[0] (MSB-first) */
+    uint64_t reg;             /* reflected register for reflected models */
+    int hw;                   /* use SSE4.2 crc32 */
+};
+
+/* ---------------------------------------------------------------------- */
+/* Tables                                                                  */
+/* ---------------------------------------------------------------------- */
+
+static uint64_t g_tab[MCK_NMODELS][8][256];
+static pthread_once_t g_once[MCK_NMODELS] = {
+#define MCK_ONCE_INIT PTHREAD_ONCE_INIT
+    MCK_ONCE_INIT, MCK_ONCE_INIT, MCK_ONCE_INIT, MCK_ONCE_INIT, MCK_ONCE_INIT, MCK_ONCE_INIT,
+    MCK_ONCE_INIT, MCK_ONCE_INIT, MCK_ONCE_INIT, MCK_ONCE_INIT, MCK_ONCE_INIT, MCK_ONCE_INIT,
+};
+static int g_init_idx_dummy;
+
+static uint64_t
+mask_of(int w)
+{
+    return w == 64 ? ~0ULL : ((1ULL << w) - 1);
+}
+
+static void
+build_tables(int idx)
+{
+    const mck_model_t *m = &mck_models[idx];
+    uint64_t mask = mask_of(m->width);
+    int b, k;
+
+    if (m->reflected) {
+        uint64_t rp = mck_reflect(m->poly, m->width);
+        for (b = 0; b < 256; b++) {
+            uint64_t r = (uint64_t) b;
+            for (k = 0; k < 8; k++)
+                r = (r & 1) ? ((r >> 1) ^ rp) : (r >> 1);
+            g_tab[idx][0][b] = r & mask;
+        }
+        /* T_k[b] = Z^(k+1)(b): one more zero byte through the register */
+        for (k = 1; k < 8; k++)
+            for (b = 0; b < 256; b++) {
+                uint64_t r = g_tab[idx][k - 1][b];
+                g_tab[idx][k][b] = ((r >> 8) ^ g_tab[idx][0][r & 0xFF]) & mask;
+            }
+    } else {
+        uint64_t top = 1ULL << (m->width - 1);
+        for (b = 0; b < 256; b++) {
+            uint64_t r = (uint64_t) b << (m->width - 8);
+            for (k = 0; k < 8; k++)
+                r = (r & top) ? ((r << 1) ^ m->poly) : (r << 1);
+            g_tab[idx][0][b] = r & mask;
+        }
+    }
+}
+
+#define DEFINE_ONCE(i)                                                         \
+    static void once_##i(void) { build_tables(i); }
+DEFINE_ONCE(0)
+DEFINE_ONCE(1)
+DEFINE_ONCE(2)
+DEFINE_ONCE(3)
+DEFINE_ONCE(4)
+DEFINE_ONCE(5)
+DEFINE_ONCE(6)
+DEFINE_ONCE(7)
+DEFINE_ONCE(8)
+DEFINE_ONCE(9)
+DEFINE_ONCE(10)
+DEFINE_ONCE(11)
+static void (*const g_once_fn[MCK_NMODELS])(void) = {once_0, once_1, once_2,
+    once_3, once_4, once_5, once_6, once_7, once_8, once_9, once_10, once_11};
+
+static const uint64_t (*tables_for(int idx))[256]
+{
+    (void) g_init_idx_dummy;
+    pthread_once(&g_once[idx], g_once_fn[idx]);
+    return (const uint64_t(*)[256]) g_tab[idx];
+}
+
+/* ---------------------------------------------------------------------- */
+/* SSE4.2                                                                  */
+/* ---------------------------------------------------------------------- */
+
+#if defined(__x86_64__)
+static pthread_once_t g_hw_once = PTHREAD_ONCE_INIT;
+static int g_hw_crc32c;
+
+static void
+detect_hw(void)
+{
+    const char *env = getenv("MCHECKSUM_DISABLE_SSE42");
+    __builtin_cpu_init();
+    g_hw_crc32c = __builtin_cpu_supports("sse4.2") && !(env && env[0] == '1');
+}
+
+__attribute__((target("sse4.2"))) static uint64_t
+crc32c_hw(uint64_t c, const uint8_t *d, size_t n)
+{
+    while (n && ((uintptr_t) d & 7)) {
+        c = __builtin_ia32_crc32qi((uint32_t) c, *d++);
+        n--;
+    }
+    /* three independent streams hide the 3-cycle instruction latency */
+    while (n >= 3 * 256) {
+        uint64_t c1 = 0, c2 = 0;
+        const uint8_t *d1 = d + 256, *d2 = d + 512;
+        int i;
+        for (i = 0; i < 32; i++) {
+            uint64_t w0, w1, w2;
+            memcpy(&w0, d + 8 * i, 8);
+            memcpy(&w1, d1 + 8 * i, 8);
+            memcpy(&w2, d2 + 8 * i, 8);
+            c = __builtin_ia32_crc32di(c, w0);
+            c1 = __builtin_ia32_crc32di(c1, w1);
+            c2 = __builtin_ia32_crc32di(c2, w2);
+        }
+        /* combine: shift c over 512 bytes, c1 over 256 bytes */
+        c = mck_crc32c_shift512(c) ^ mck_crc32c_shift256(c1) ^ c2;
+        d += 768;
+        n -= 768;
+    }
+    while (n >= 8) {
+        uint64_t w;
+        memcpy(&w, d, 8);
+        c = __builtin_ia32_crc32di(c, w);
+        d += 8;
+        n -= 8;
+    }
+    while (n--)
+        c = __builtin_ia32_crc32qi((uint32_t) c, *d++);
+    return c;
+}
+#endif
+
+/* ---------------------------------------------------------------------- */
+/* Software update                                                         */
+/* ---------------------------------------------------------------------- */
+
+static uint64_t
+update_reflected(const uint64_t (*t)[256], uint64_t reg, const uint8_t *d, size_t n)
+{
+    while (n && ((uintptr_t) d & 7)) {
+        reg = (reg >> 8) ^ t[0][(reg ^ *d++) & 0xFF];
+        n--;
+    }
+    while (n >= 8) {
+        uint64_t x;
+        memcpy(&x, d, 8);
+        x ^= reg;
+        reg = t[7][x & 0xFF] ^ t[6][(x >> 8) & 0xFF] ^ t[5][(x >> 16) & 0xFF] ^
+              t[4][(x >> 24) & 0xFF] ^ t[3][(x >> 32) & 0xFF] ^
+              t[2][(x >> 40) & 0xFF] ^ t[1][(x >> 48) & 0xFF] ^ t[0][x >> 56];
+        d += 8;
+        n -= 8;
+    }
+    while (n--)
+        reg = (reg >> 8) ^ t[0][(reg ^ *d++) & 0xFF];
+    return reg;
+}
+
+static uint64_t
+update_msb(const mck_model_t *m, const uint64_t *t, uint64_t reg, const uint8_t *d, size_t n)
+{
+    const uint64_t mask = mask_of(m->width);
+    const int sh = m->width - 8;
+
+    while (n--)
+        reg = ((reg << 8) ^ t[((reg >> sh) ^ *d++) & 0xFF]) & mask;
+    return reg;
+}
+
+/* ---------------------------------------------------------------------- */
+/* Public API                                                              */
+/* ---------------------------------------------------------------------- */
+
+static void
+log_error(const char *fmt, const char *arg)
+{
+    const char *lvl = getenv("MCHECKSUM_LOG_LEVEL");
+    if (lvl && (strcmp(lvl, "none") == 0 || strcmp(lvl, "0") == 0))
+        return;
+    fprintf(stderr, "# mchecksum error: ");
+    fprintf(stderr, fmt, arg ? arg : "(null)");
+    fprintf(stderr, "\n");
+}
+
+int
+mchecksum_init(const char *hash_method, mchecksum_object_t *checksum)
+{
+    struct mchecksum_object *obj;
+    int idx;
+
+    if (!checksum) {
+        log_error("NULL checksum pointer passed to init (%s)", hash_method);
+        return MCHECKSUM_FAIL;
+    }
+    idx = mck_model_index(hash_method);
+    if (idx < 0) {
+        log_error("unknown hash method \"%s\"", hash_method);
+        return MCHECKSUM_FAIL;
+    }
+    obj = (struct mchecksum_object *) calloc(1, sizeof(*obj));
+    if (!obj) {
+        log_error("could not allocate checksum object (%s)", hash_method);
+        return MCHECKSUM_FAIL;
+    }
+    obj->m = &mck_models[idx];
+    obj->t = tables_for(idx);
+#if defined(__x86_64__)
+    if (strcmp(obj->m->name, "crc32c") == 0) {
+        pthread_once(&g_hw_once, detect_hw);
+        obj->hw = g_hw_crc32c;
+    }
+#endif
+    mchecksum_reset(obj);
+    *checksum = obj;
+    return MCHECKSUM_SUCCESS;
+}
+
+int
+mchecksum_destroy(mchecksum_object_t checksum)
+{
+    free(checksum); /* NULL is a no-op, as src/mercury_proc.c:93,136 need */
+    return MCHECKSUM_SUCCESS;
+}
+
+int
+mchecksum_reset(mchecksum_object_t checksum)
+{
+    if (!checksum)
+        return MCHECKSUM_FAIL;
+    checksum->reg = checksum->m->reflected
+                        ? mck_reflect(checksum->m->init, checksum->m->width)
+                        : (checksum->m->init & mask_of(checksum->m->width));
+    return MCHECKSUM_SUCCESS;
+}
+
+size_t
+mchecksum_get_size(mchecksum_object_t checksum)
+{
+    if (!checksum)
+        return 0;
+    return (size_t) (checksum->m->width / 8);
+}
+
+int
+mchecksum_get(mchecksum_object_t checksum, void *buf, size_t size, int finalize)
+{
+    uint64_t v;
+
+    (void) finalize; /* CRC get is non-destructive; both forms return the
+                        finished value (Mercury only passes FINALIZE) */
+    if (!checksum || !buf)
+        return MCHECKSUM_FAIL;
+    if (size < mchecksum_get_size(checksum))
+        return MCHECKSUM_FAIL;
+    v = (checksum->reg ^ checksum->m->xorout) & mask_of(checksum->m->width);
+    switch (checksum->m->width) {
+        case 16: {
+            uint16_t x = (uint16_t) v;
+            memcpy(buf, &x, 2);
+            break;
+        }
+        case 32: {
+            uint32_t x = (uint32_t) v;
+            memcpy(buf, &x, 4);
+            break;
+        }
+        default:
+            memcpy(buf, &v, 8);
+            break;
+    }
+    return MCHECKSUM_SUCCESS;
+}
+
+int
+mchecksum_update(mchecksum_object_t checksum, const void *data, size_t size)
+{
+    const uint8_t *d = (const uint8_t *) data;
+
+    if (!checksum || (!data && size))
+        return MCHECKSUM_FAIL;
+    if (!size)
+        return MCHECKSUM_SUCCESS;
+#if defined(__x86_64__)
+    if (checksum->hw) {
+        checksum->reg = crc32c_hw(checksum->reg, d, size) & 0xFFFFFFFFULL;
+        return MCHECKSUM_SUCCESS;
+    }
+#endif
+    if (checksum->m->reflected)
+        checksum->reg = update_reflected(checksum->t, checksum->reg, d, size);
+    else
+        checksum->reg = update_msb(checksum->m, checksum->t[0], checksum->reg, d, size);
+    return MCHECKSUM_SUCCESS;
+}

@@ -1,0 +1,724 @@
+// mchecksum_gpu.hip -- MI355X (gfx950) batch CRC kernels behind the C ABI in
+// include/mchecksum_gpu.h.
+//
+// What is computed.  For each payload i, the value mchecksum_get() returns
+// after mchecksum_update(payload_i) -- the CRC Mercury stores in the HG header
+// for a serialized proc buffer (src/mercury_proc.c:358-406,
+// src/mercury.c:699-707, src/mercury_header.c:111-112).
+//
+// How (algebra in crc_gpu_layout.h; validated by tests/native/kernel_emulator):
+//  * A payload is covered by a 16-byte-aligned window whose END is aligned to
+//    the step grid; G lanes (one group) cover one step of 16*G bytes, each lane
+//    one coalesced dwordx4 (so a G = 64 wave reads 1 KiB per instruction).
+//  * Every W-bit word slot of a lane is an independent sub-stream with a
+//    uniform stride of 16*G bytes, so "advance by the stride" is folded into
+//    the lookup tables: s <- F(s ^ w) costs 4 byte lookups (CRC-32C) or 16
+//    nibble lookups (CRC-64) and no shift/multiply.
+//  * Lookup tables live in LDS, replicated 32x so lane l always hits bank
+//    l % 32: every ds_read_b32/b64 is conflict-free.  Addresses are formed by
+//    one v_perm_b32 per lookup (byte -> entry stride 256 B, lane copy in the
+//    low byte).
+//  * Sub-streams are combined by a tree (in-lane, then xor-shuffles across the
+//    group) whose level operators Z^-(2^k * W/8) are nibble tables in LDS;
+//    Z^-t removes the t pad bytes after the payload end.
+//  * One 1024-thread workgroup per CU (the replicated tables take 128 KiB of
+//    the 160 KiB LDS), persistent over the batch: waves stride over payloads.
+// No MFMA: this is HBM-bound byte scanning; the roofline is HBM read bandwidth.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+
+#include "crc_gpu_layout.h"
+#include "mchecksum_gpu.h"
+#include "mchecksum_models.h"
+
+namespace {
+
+constexpr int kBlock = 1024;  // 16 waves: 4 per SIMD
+constexpr int kWavesPerBlock = kBlock / 64;
+constexpr int kRing = 4;  // dwordx4 pieces in flight per lane
+
+// CRC-32C LDS map: [0,128K) main byte tables x32 copies; then op nibble tables.
+constexpr uint32_t kL32Main = 131072;
+constexpr uint32_t kL32Bytes = kL32Main + CRC32_NOPS_MAX * 512;
+// CRC-64 LDS map: [0,64K) main nibble tables x32 copies; then op nibble tables.
+constexpr uint32_t kL64Main = 65536;
+constexpr uint32_t kL64Bytes = kL64Main + CRC64_NOPS_MAX * 2048;
+
+enum Mode : int { kFixedAligned = 0, kFixedGeneric = 1, kOffsets = 2 };
+
+struct BatchArgs {
+    const uint8_t *base;
+    const uint64_t *offsets;
+    uint64_t stride, len, count;
+    void *out;
+    const void *expected;
+    uint8_t *status;
+    uint32_t *mismatches;
+    const void *pack;
+};
+
+#ifdef MCHECKSUM_NT_LOADS
+__device__ __forceinline__ uint4 ld16(const uint4 *p) { return __builtin_nontemporal_load(p); }
+#else
+__device__ __forceinline__ uint4 ld16(const uint4 *p) { return *p; }
+#endif
+
+__device__ __forceinline__ uint32_t lds32(const uint8_t *lds, uint32_t a) {
+    return *reinterpret_cast<const uint32_t *>(lds + a);
+}
+__device__ __forceinline__ uint64_t lds64(const uint8_t *lds, uint32_t a) {
+    return *reinterpret_cast<const uint64_t *>(lds + a);
+}
+
+// ---------------------------------------------------------------- CRC-32C --
+
+// s' = Z^(16G)(x): main[p][byte_p(x)], tables p=0,1 in LDS region 0 (lc0),
+// p=2,3 in region 1 (lc1 has +64 KiB in its byte 2); odd p at +128 B.
+__device__ __forceinline__ uint32_t f32(const uint8_t *lds, uint32_t x, uint32_t lc0, uint32_t lc1) {
+    const uint32_t a0 = __builtin_amdgcn_perm(x, lc0, 0x0C020400u);
+    const uint32_t a1 = __builtin_amdgcn_perm(x, lc0, 0x0C020500u);
+    const uint32_t a2 = __builtin_amdgcn_perm(x, lc1, 0x0C020600u);
+    const uint32_t a3 = __builtin_amdgcn_perm(x, lc1, 0x0C020700u);
+    return lds32(lds, a0) ^ lds32(lds, a1 + 128) ^ lds32(lds, a2) ^ lds32(lds, a3 + 128);
+}
+
+__device__ __forceinline__ uint32_t op32(const uint8_t *lds, uint32_t o, uint32_t x) {
+    const uint32_t base = kL32Main + o * 512;
+    uint32_t r = 0;
+#pragma unroll
+    for (int h = 0; h < 8; h++) r ^= lds32(lds, base + h * 64 + (((x >> (4 * h)) & 15u) << 2));
+    return r;
+}
+
+__device__ __forceinline__ uint32_t mask32(uint32_t w, int64_t lo, int64_t len, uint32_t init) {
+    if (lo >= len || lo <= -4) return 0;
+    const int sc = lo < 0 ? (int)(-lo) : 0;
+    const int64_t e = lo + 4 - len;
+    const int ec = e > 0 ? (int)e : 0;
+    w &= (0xFFFFFFFFu << (8 * sc)) & (0xFFFFFFFFu >> (8 * ec));
+    if (len >= 4 && lo < 4) w ^= lo >= 0 ? (init << (8 * (int)lo)) : (init >> (8 * (int)(-lo)));
+    return w;
+}
+
+template <int LOG2G>
+__device__ __forceinline__ uint32_t combine32(const uint8_t *lds, uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3,
+                                              uint32_t gl) {
+    uint32_t x = s0 ^ op32(lds, 0, s1);
+    const uint32_t y = s2 ^ op32(lds, 0, s3);
+    x ^= op32(lds, 1, y);
+#pragma unroll
+    for (int k = 0; k < LOG2G; k++) {
+        const uint32_t other = __shfl_xor(x, 1 << k, 64);
+        const bool bit = (gl >> k) & 1u;
+        const uint32_t lo = bit ? other : x, hi = bit ? x : other;
+        x = lo ^ op32(lds, 2 + k, hi);
+    }
+    return x;
+}
+
+__device__ void fill_lds32(uint8_t *lds, const crc32_gpu_pack_t *pk) {
+    uint32_t *l = reinterpret_cast<uint32_t *>(lds);
+    for (uint32_t d = threadIdx.x; d < 32768u; d += kBlock) {
+        const uint32_t region = d >> 14, e = (d >> 6) & 255u, half = (d >> 5) & 1u;
+        l[d] = pk->main[2 * region + half][e];
+    }
+    const uint32_t *ops = &pk->ops[0][0][0];
+    const uint32_t nops = pk->nops * 128u;
+    for (uint32_t d = threadIdx.x; d < nops; d += kBlock) l[kL32Main / 4 + d] = ops[d];
+}
+
+// Aligned fixed-size payload: base 16-B aligned, len = K * 16G, no masking,
+// no pad bytes (tail op is the identity and is skipped).
+template <int LOG2G>
+__device__ __forceinline__ uint32_t payload32_aligned(const uint8_t *lds, const uint8_t *p, uint64_t K, uint32_t gl,
+                                                      uint32_t lc0, uint32_t lc1, uint32_t init) {
+    constexpr int G = 1 << LOG2G;
+    const uint4 *src = reinterpret_cast<const uint4 *>(p) + gl;
+    uint32_t s0 = gl == 0 ? init : 0u, s1 = 0, s2 = 0, s3 = 0;
+    uint4 ring[kRing];
+#pragma unroll
+    for (int u = 0; u < kRing; u++) ring[u] = (uint64_t)u < K ? ld16(src + (uint64_t)u * G) : make_uint4(0, 0, 0, 0);
+    for (uint64_t k = 0; k < K; k += kRing) {
+#pragma unroll
+        for (int u = 0; u < kRing; u++) {
+            const uint4 v = ring[u];
+            const uint64_t kn = k + u + kRing;
+            if (kn < K) ring[u] = ld16(src + kn * G);
+            if (k + u < K) {
+                s0 = f32(lds, s0 ^ v.x, lc0, lc1);
+                s1 = f32(lds, s1 ^ v.y, lc0, lc1);
+                s2 = f32(lds, s2 ^ v.z, lc0, lc1);
+                s3 = f32(lds, s3 ^ v.w, lc0, lc1);
+            }
+        }
+    }
+    return combine32<LOG2G>(lds, s0, s1, s2, s3, gl);
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_max(T v) {
+#pragma unroll
+    for (int k = 1; k < 64; k <<= 1) {
+        const T o = __shfl_xor(v, k, 64);
+        v = o > v ? o : v;
+    }
+    return v;
+}
+
+// Any alignment, any length (0 included).  Per-lane window; the wave loops to
+// the largest step count of its groups.
+template <int LOG2G>
+__device__ __forceinline__ uint32_t payload32_generic(const uint8_t *lds, const crc32_gpu_pack_t *pk,
+                                                      const uint8_t *p, uint64_t len, uint32_t gl, uint32_t lc0,
+                                                      uint32_t lc1) {
+    constexpr int G = 1 << LOG2G;
+    constexpr int64_t step = 16 * G;
+    const uint32_t init = pk->init;
+    const uint64_t sa = reinterpret_cast<uint64_t>(p), ea = sa + len;
+    const uint64_t a0 = sa & ~15ull, a1 = (ea + 15) & ~15ull;
+    const int64_t W = (int64_t)(a1 - a0);
+    const int64_t K = (W + step - 1) >> (4 + LOG2G);
+    const int64_t r0 = W - K * step;
+    const int64_t hs = (int64_t)(sa - a0), he = (int64_t)(ea - a0);
+    const int64_t ilen = (int64_t)len;
+    const int64_t kmax = LOG2G == 6 ? K : wave_max(K);
+    const int64_t lane_off = 16 * (int64_t)gl;
+
+    auto fetch = [&](int64_t k) -> uint4 {
+        const int64_t pc = r0 + k * step + lane_off;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (k < K && pc >= 0) v = ld16(reinterpret_cast<const uint4 *>(a0 + (uint64_t)pc));
+        return v;
+    };
+
+    uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+    uint4 ring[kRing];
+#pragma unroll
+    for (int u = 0; u < kRing; u++) ring[u] = fetch(u);
+    for (int64_t k = 0; k < kmax; k += kRing) {
+#pragma unroll
+        for (int u = 0; u < kRing; u++) {
+            uint4 v = ring[u];
+            const int64_t kk = k + u;
+            ring[u] = fetch(kk + kRing);
+            if (kk < K) {
+                const int64_t pc = r0 + kk * step + lane_off;
+                if (!(pc >= hs + 4 && pc + 16 <= he)) {
+                    const int64_t lo = pc - hs;
+                    v.x = mask32(v.x, lo, ilen, init);
+                    v.y = mask32(v.y, lo + 4, ilen, init);
+                    v.z = mask32(v.z, lo + 8, ilen, init);
+                    v.w = mask32(v.w, lo + 12, ilen, init);
+                }
+                s0 = f32(lds, s0 ^ v.x, lc0, lc1);
+                s1 = f32(lds, s1 ^ v.y, lc0, lc1);
+                s2 = f32(lds, s2 ^ v.z, lc0, lc1);
+                s3 = f32(lds, s3 ^ v.w, lc0, lc1);
+            }
+        }
+    }
+    uint32_t x = combine32<LOG2G>(lds, s0, s1, s2, s3, gl);
+    x = op32(lds, 2 + LOG2G + (uint32_t)(a1 - ea), x);
+    if (len < 4) x ^= pk->zinit[len];
+    return x;
+}
+
+// Byte-balanced static partition of an offsets batch: wave w owns payloads
+// whose start offset lies in [off0 + total*w/nw, off0 + total*(w+1)/nw).
+__device__ __forceinline__ uint64_t lower_bound_u64(const uint64_t *a, uint64_t n, uint64_t key) {
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint64_t mid = lo + ((hi - lo) >> 1);
+        if (a[mid] < key) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__device__ __forceinline__ void wave_range(const uint64_t *off, uint64_t count, uint32_t wave, uint32_t nw,
+                                           uint64_t *first, uint64_t *last) {
+    const uint64_t o0 = off[0], total = off[count] - o0;
+    const uint64_t q = total / nw, r = total % nw;
+    const uint64_t lo = o0 + q * wave + (r * wave) / nw;
+    const uint64_t hi = o0 + q * (wave + 1) + (r * (wave + 1)) / nw;
+    *first = wave == 0 ? 0 : lower_bound_u64(off, count, lo);
+    *last = wave + 1 == nw ? count : lower_bound_u64(off, count, hi);
+}
+
+template <typename T, bool VERIFY>
+__device__ __forceinline__ void emit(const BatchArgs &a, uint64_t p, T v) {
+    if (VERIFY) {
+        const bool bad = reinterpret_cast<const T *>(a.expected)[p] != v;
+        if (a.status) a.status[p] = bad ? 1 : 0;
+        if (bad && a.mismatches) atomicAdd(a.mismatches, 1u);
+    } else {
+        reinterpret_cast<T *>(a.out)[p] = v;
+    }
+}
+
+template <int LOG2G, int MODE, bool VERIFY>
+__global__ __launch_bounds__(kBlock, 1) void crc32c_batch_kernel(BatchArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kL32Bytes];
+    const crc32_gpu_pack_t *pk = reinterpret_cast<const crc32_gpu_pack_t *>(a.pack);
+    fill_lds32(lds, pk);
+    __syncthreads();
+
+    constexpr int PPW = 64 >> LOG2G;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t gl = lane & ((1u << LOG2G) - 1u), grp = lane >> LOG2G;
+    const uint32_t lc0 = (lane & 31u) << 2, lc1 = lc0 | 0x10000u;
+    const uint32_t xorout = pk->xorout;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
+    const uint32_t nw = gridDim.x * kWavesPerBlock;
+
+    if (MODE == kOffsets) {
+        uint64_t first, last;
+        wave_range(a.offsets, a.count, wave, nw, &first, &last);
+        for (uint64_t p = first; p < last; p++) {
+            const uint64_t o = a.offsets[p];
+            const uint32_t x = payload32_generic<LOG2G>(lds, pk, a.base + o, a.offsets[p + 1] - o, gl, lc0, lc1);
+            if (gl == 0) emit<uint32_t, VERIFY>(a, p, x ^ xorout);
+        }
+        return;
+    }
+    for (uint64_t pb = (uint64_t)wave * PPW; pb < a.count; pb += (uint64_t)nw * PPW) {
+        const uint64_t p = pb + grp;
+        const bool act = p < a.count;
+        const uint64_t pc = act ? p : a.count - 1;
+        uint32_t x;
+        if (MODE == kFixedAligned)
+            x = payload32_aligned<LOG2G>(lds, a.base + pc * a.stride, a.len >> (4 + LOG2G), gl, lc0, lc1, pk->init);
+        else
+            x = payload32_generic<LOG2G>(lds, pk, a.base + pc * a.stride, a.len, gl, lc0, lc1);
+        if (act && gl == 0) emit<uint32_t, VERIFY>(a, p, x ^ xorout);
+    }
+}
+
+// ----------------------------------------------------------------- CRC-64 --
+
+// s' = Z^(16G)(x) from 16 nibble tables; table 2p+h at (2p+h)*4 KiB, entry v
+// at v*256 B, lane copy at (lane%32)*8 B.
+__device__ __forceinline__ uint64_t f64(const uint8_t *lds, uint64_t x, uint32_t lc) {
+    const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
+    const uint32_t n0 = xl & 0x0F0F0F0Fu, n1 = (xl >> 4) & 0x0F0F0F0Fu;
+    const uint32_t n2 = xh & 0x0F0F0F0Fu, n3 = (xh >> 4) & 0x0F0F0F0Fu;
+    uint64_t r = 0;
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+        const uint32_t sel = 0x0C0C0400u | ((uint32_t)b << 8);
+        r ^= lds64(lds, __builtin_amdgcn_perm(n0, lc, sel) + (2 * b + 0) * 4096);
+        r ^= lds64(lds, __builtin_amdgcn_perm(n1, lc, sel) + (2 * b + 1) * 4096);
+        r ^= lds64(lds, __builtin_amdgcn_perm(n2, lc, sel) + (2 * (b + 4) + 0) * 4096);
+        r ^= lds64(lds, __builtin_amdgcn_perm(n3, lc, sel) + (2 * (b + 4) + 1) * 4096);
+    }
+    return r;
+}
+
+__device__ __forceinline__ uint64_t op64(const uint8_t *lds, uint32_t o, uint64_t x) {
+    const uint32_t base = kL64Main + o * 2048;
+    uint64_t r = 0;
+#pragma unroll
+    for (int h = 0; h < 16; h++) r ^= lds64(lds, base + h * 128 + (uint32_t)(((x >> (4 * h)) & 15u) << 3));
+    return r;
+}
+
+__device__ __forceinline__ uint64_t mask64(uint64_t w, int64_t lo, int64_t len, uint64_t init) {
+    if (lo >= len || lo <= -8) return 0;
+    const int sc = lo < 0 ? (int)(-lo) : 0;
+    const int64_t e = lo + 8 - len;
+    const int ec = e > 0 ? (int)e : 0;
+    w &= (~0ull << (8 * sc)) & (~0ull >> (8 * ec));
+    if (len >= 8 && lo < 8) w ^= lo >= 0 ? (init << (8 * (int)lo)) : (init >> (8 * (int)(-lo)));
+    return w;
+}
+
+template <int LOG2G>
+__device__ __forceinline__ uint64_t combine64(const uint8_t *lds, uint64_t s0, uint64_t s1, uint32_t gl) {
+    uint64_t x = s0 ^ op64(lds, 0, s1);
+#pragma unroll
+    for (int k = 0; k < LOG2G; k++) {
+        const uint64_t other = __shfl_xor(x, 1 << k, 64);
+        const bool bit = (gl >> k) & 1u;
+        const uint64_t lo = bit ? other : x, hi = bit ? x : other;
+        x = lo ^ op64(lds, 1 + k, hi);
+    }
+    return x;
+}
+
+__device__ void fill_lds64(uint8_t *lds, const crc64_gpu_pack_t *pk) {
+    uint64_t *l = reinterpret_cast<uint64_t *>(lds);
+    for (uint32_t d = threadIdx.x; d < 8192u; d += kBlock) l[d] = pk->main[d >> 9][(d >> 5) & 15u];
+    const uint64_t *ops = &pk->ops[0][0][0];
+    const uint32_t nops = pk->nops * 256u;
+    for (uint32_t d = threadIdx.x; d < nops; d += kBlock) l[kL64Main / 8 + d] = ops[d];
+}
+
+template <int LOG2G>
+__device__ __forceinline__ uint64_t payload64_aligned(const uint8_t *lds, const uint8_t *p, uint64_t K, uint32_t gl,
+                                                      uint32_t lc, uint64_t init) {
+    constexpr int G = 1 << LOG2G;
+    const uint4 *src = reinterpret_cast<const uint4 *>(p) + gl;
+    uint64_t s0 = gl == 0 ? init : 0ull, s1 = 0;
+    uint4 ring[kRing];
+#pragma unroll
+    for (int u = 0; u < kRing; u++) ring[u] = (uint64_t)u < K ? ld16(src + (uint64_t)u * G) : make_uint4(0, 0, 0, 0);
+    for (uint64_t k = 0; k < K; k += kRing) {
+#pragma unroll
+        for (int u = 0; u < kRing; u++) {
+            const uint4 v = ring[u];
+            const uint64_t kn = k + u + kRing;
+            if (kn < K) ring[u] = ld16(src + kn * G);
+            if (k + u < K) {
+                s0 = f64(lds, s0 ^ ((uint64_t)v.y << 32 | v.x), lc);
+                s1 = f64(lds, s1 ^ ((uint64_t)v.w << 32 | v.z), lc);
+            }
+        }
+    }
+    return combine64<LOG2G>(lds, s0, s1, gl);
+}
+
+template <int LOG2G>
+__device__ __forceinline__ uint64_t payload64_generic(const uint8_t *lds, const crc64_gpu_pack_t *pk,
+                                                      const uint8_t *p, uint64_t len, uint32_t gl, uint32_t lc) {
+    constexpr int G = 1 << LOG2G;
+    constexpr int64_t step = 16 * G;
+    const uint64_t init = pk->init;
+    const uint64_t sa = reinterpret_cast<uint64_t>(p), ea = sa + len;
+    const uint64_t a0 = sa & ~15ull, a1 = (ea + 15) & ~15ull;
+    const int64_t W = (int64_t)(a1 - a0);
+    const int64_t K = (W + step - 1) >> (4 + LOG2G);
+    const int64_t r0 = W - K * step;
+    const int64_t hs = (int64_t)(sa - a0), he = (int64_t)(ea - a0);
+    const int64_t ilen = (int64_t)len;
+    const int64_t kmax = LOG2G == 6 ? K : wave_max(K);
+    const int64_t lane_off = 16 * (int64_t)gl;
+
+    auto fetch = [&](int64_t k) -> uint4 {
+        const int64_t pc = r0 + k * step + lane_off;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (k < K && pc >= 0) v = ld16(reinterpret_cast<const uint4 *>(a0 + (uint64_t)pc));
+        return v;
+    };
+
+    uint64_t s0 = 0, s1 = 0;
+    uint4 ring[kRing];
+#pragma unroll
+    for (int u = 0; u < kRing; u++) ring[u] = fetch(u);
+    for (int64_t k = 0; k < kmax; k += kRing) {
+#pragma unroll
+        for (int u = 0; u < kRing; u++) {
+            const uint4 v = ring[u];
+            const int64_t kk = k + u;
+            ring[u] = fetch(kk + kRing);
+            if (kk < K) {
+                const int64_t pc = r0 + kk * step + lane_off;
+                uint64_t w0 = (uint64_t)v.y << 32 | v.x, w1 = (uint64_t)v.w << 32 | v.z;
+                if (!(pc >= hs + 8 && pc + 16 <= he)) {
+                    const int64_t lo = pc - hs;
+                    w0 = mask64(w0, lo, ilen, init);
+                    w1 = mask64(w1, lo + 8, ilen, init);
+                }
+                s0 = f64(lds, s0 ^ w0, lc);
+                s1 = f64(lds, s1 ^ w1, lc);
+            }
+        }
+    }
+    uint64_t x = combine64<LOG2G>(lds, s0, s1, gl);
+    x = op64(lds, 1 + LOG2G + (uint32_t)(a1 - ea), x);
+    if (len < 8) x ^= pk->zinit[len];
+    return x;
+}
+
+template <int LOG2G, int MODE, bool VERIFY>
+__global__ __launch_bounds__(kBlock, 1) void crc64_batch_kernel(BatchArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kL64Bytes];
+    const crc64_gpu_pack_t *pk = reinterpret_cast<const crc64_gpu_pack_t *>(a.pack);
+    fill_lds64(lds, pk);
+    __syncthreads();
+
+    constexpr int PPW = 64 >> LOG2G;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t gl = lane & ((1u << LOG2G) - 1u), grp = lane >> LOG2G;
+    const uint32_t lc = (lane & 31u) << 3;
+    const uint64_t xorout = pk->xorout;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
+    const uint32_t nw = gridDim.x * kWavesPerBlock;
+
+    if (MODE == kOffsets) {
+        uint64_t first, last;
+        wave_range(a.offsets, a.count, wave, nw, &first, &last);
+        for (uint64_t p = first; p < last; p++) {
+            const uint64_t o = a.offsets[p];
+            const uint64_t x = payload64_generic<LOG2G>(lds, pk, a.base + o, a.offsets[p + 1] - o, gl, lc);
+            if (gl == 0) emit<uint64_t, VERIFY>(a, p, x ^ xorout);
+        }
+        return;
+    }
+    for (uint64_t pb = (uint64_t)wave * PPW; pb < a.count; pb += (uint64_t)nw * PPW) {
+        const uint64_t p = pb + grp;
+        const bool act = p < a.count;
+        const uint64_t pc = act ? p : a.count - 1;
+        uint64_t x;
+        if (MODE == kFixedAligned)
+            x = payload64_aligned<LOG2G>(lds, a.base + pc * a.stride, a.len >> (4 + LOG2G), gl, lc, pk->init);
+        else
+            x = payload64_generic<LOG2G>(lds, pk, a.base + pc * a.stride, a.len, gl, lc);
+        if (act && gl == 0) emit<uint64_t, VERIFY>(a, p, x ^ xorout);
+    }
+}
+
+// ------------------------------------------------------------ host side ----
+
+thread_local char t_err[256] = "";
+
+int set_err(int rc, const char *fmt, const char *a = "", int b = 0) {
+    snprintf(t_err, sizeof(t_err), fmt, a, b);
+    return rc;
+}
+
+int hip_err(hipError_t e, const char *what) {
+    snprintf(t_err, sizeof(t_err), "%s: %s", what, hipGetErrorString(e));
+    return MCHECKSUM_GPU_EHIP;
+}
+
+constexpr int kMaxDev = 64;
+
+struct DevCtx {
+    bool init = false;
+    int cus = 0;
+    void *pack[MCK_NMODELS][CRC_GPU_MAX_LOG2G + 1] = {};
+};
+
+std::mutex g_mu;
+DevCtx g_dev[kMaxDev];
+
+// Method -> (model index, width) for GPU-capable (reflected 32/64-bit) models.
+int gpu_model(const char *method, int *width) {
+    const int idx = mck_model_index(method);
+    if (idx < 0) return -1;
+    const mck_model_t &m = mck_models[idx];
+    if (!m.reflected || (m.width != 32 && m.width != 64)) return -2;
+    *width = m.width;
+    return idx;
+}
+
+int device_ctx(DevCtx **out) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return hip_err(e, "hipGetDevice");
+    if (dev < 0 || dev >= kMaxDev) return set_err(MCHECKSUM_GPU_ENODEV, "device id %s%d out of range", "", dev);
+    DevCtx &c = g_dev[dev];
+    if (!c.init) {
+        int cus = 0;
+        e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (e != hipSuccess) return hip_err(e, "hipDeviceGetAttribute");
+        c.cus = cus > 0 ? cus : 1;
+        c.init = true;
+    }
+    *out = &c;
+    return 0;
+}
+
+// Returns the device table pack for (model, log2g), building it on first use.
+int get_pack(DevCtx *c, int idx, int log2g, const void **pack) {
+    if (c->pack[idx][log2g]) {
+        *pack = c->pack[idx][log2g];
+        return 0;
+    }
+    const mck_model_t &m = mck_models[idx];
+    crc_rmodel_t rm;
+    rm.width = m.width;
+    rm.rpoly = mck_reflect(m.poly, m.width);
+    rm.rinit = mck_reflect(m.init, m.width);
+    rm.xorout = m.xorout;
+    void *host = nullptr;
+    size_t bytes = 0;
+    int rc;
+    if (m.width == 32) {
+        bytes = sizeof(crc32_gpu_pack_t);
+        host = calloc(1, bytes);
+        rc = host ? crc32_gpu_pack_build(&rm, log2g, (crc32_gpu_pack_t *)host) : -1;
+    } else {
+        bytes = sizeof(crc64_gpu_pack_t);
+        host = calloc(1, bytes);
+        rc = host ? crc64_gpu_pack_build(&rm, log2g, (crc64_gpu_pack_t *)host) : -1;
+    }
+    if (rc != 0) {
+        free(host);
+        return set_err(MCHECKSUM_GPU_EINVAL, "table build failed for %s%d", m.name, log2g);
+    }
+    void *d = nullptr;
+    hipError_t e = hipMalloc(&d, bytes);
+    if (e == hipSuccess) e = hipMemcpy(d, host, bytes, hipMemcpyHostToDevice);
+    free(host);
+    if (e != hipSuccess) {
+        if (d) (void)hipFree(d);
+        return hip_err(e, "table upload");
+    }
+    c->pack[idx][log2g] = d;
+    *pack = d;
+    return 0;
+}
+
+int choose_log2g(size_t len) {
+    const char *env = getenv("MCHECKSUM_GPU_LOG2G");
+    if (env && env[0]) {
+        const int v = atoi(env);
+        if (v >= 0 && v <= CRC_GPU_MAX_LOG2G) return v;
+    }
+    // Aim for >= 16 steps per payload, at most 64 lanes per payload.
+    const size_t target = len / 256;
+    int lg = 0;
+    while (lg < CRC_GPU_MAX_LOG2G && ((size_t)1 << (lg + 1)) <= target) lg++;
+    return lg;
+}
+
+typedef void (*kern_t)(BatchArgs);
+
+template <int W, int LOG2G, int MODE, bool VERIFY>
+kern_t kernel_ptr() {
+    if constexpr (W == 32) return crc32c_batch_kernel<LOG2G, MODE, VERIFY>;
+    else return crc64_batch_kernel<LOG2G, MODE, VERIFY>;
+}
+
+template <int W>
+kern_t pick_fixed(int log2g, bool aligned) {
+    switch (log2g) {
+        case 0: return aligned ? kernel_ptr<W, 0, kFixedAligned, false>() : kernel_ptr<W, 0, kFixedGeneric, false>();
+        case 1: return aligned ? kernel_ptr<W, 1, kFixedAligned, false>() : kernel_ptr<W, 1, kFixedGeneric, false>();
+        case 2: return aligned ? kernel_ptr<W, 2, kFixedAligned, false>() : kernel_ptr<W, 2, kFixedGeneric, false>();
+        case 3: return aligned ? kernel_ptr<W, 3, kFixedAligned, false>() : kernel_ptr<W, 3, kFixedGeneric, false>();
+        case 4: return aligned ? kernel_ptr<W, 4, kFixedAligned, false>() : kernel_ptr<W, 4, kFixedGeneric, false>();
+        case 5: return aligned ? kernel_ptr<W, 5, kFixedAligned, false>() : kernel_ptr<W, 5, kFixedGeneric, false>();
+        default: return aligned ? kernel_ptr<W, 6, kFixedAligned, false>() : kernel_ptr<W, 6, kFixedGeneric, false>();
+    }
+}
+
+int launch(kern_t k, const BatchArgs &a, unsigned blocks, void *stream) {
+    hipLaunchKernelGGL(k, dim3(blocks), dim3(kBlock), 0, (hipStream_t)stream, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_err(e, "kernel launch");
+    return MCHECKSUM_GPU_OK;
+}
+
+unsigned grid_for(const DevCtx *c, uint64_t waves_needed) {
+    uint64_t blocks = (waves_needed + kWavesPerBlock - 1) / kWavesPerBlock;
+    if (blocks > (uint64_t)c->cus) blocks = (uint64_t)c->cus;
+    return blocks ? (unsigned)blocks : 1u;
+}
+
+int prologue(const char *method, int log2g, int *width, DevCtx **c, const void **pack) {
+    int idx = gpu_model(method, width);
+    if (idx == -1) return set_err(MCHECKSUM_GPU_EMETHOD, "unknown hash method \"%s\"%d", method ? method : "(null)");
+    if (idx < 0) return set_err(MCHECKSUM_GPU_EMETHOD, "method \"%s\" has no GPU kernel (reflected 32/64-bit only)%d", method);
+    std::lock_guard<std::mutex> lk(g_mu);
+    int rc = device_ctx(c);
+    if (rc) return rc;
+    return get_pack(*c, idx, log2g, pack);
+}
+
+int do_offsets(const char *method, const void *base, const uint64_t *offsets, size_t count, void *out,
+               const void *expected, uint8_t *status, uint32_t *mism, void *stream, bool verify) {
+    if ((!base && count) || !offsets || (!verify && !out && count) || (verify && !expected))
+        return set_err(MCHECKSUM_GPU_EINVAL, "NULL pointer argument%s%d");
+    if (!mchecksum_gpu_available()) return set_err(MCHECKSUM_GPU_ENODEV, "no HIP device%s%d");
+    int width = 0;
+    DevCtx *c = nullptr;
+    const void *pack = nullptr;
+    int rc = prologue(method, CRC_GPU_MAX_LOG2G, &width, &c, &pack);
+    if (rc) return rc;
+    if (count == 0) return MCHECKSUM_GPU_OK;
+    BatchArgs a{};
+    a.base = (const uint8_t *)base;
+    a.offsets = offsets;
+    a.count = count;
+    a.out = out;
+    a.expected = expected;
+    a.status = status;
+    a.mismatches = mism;
+    a.pack = pack;
+    kern_t k;
+    if (width == 32)
+        k = verify ? kernel_ptr<32, 6, kOffsets, true>() : kernel_ptr<32, 6, kOffsets, false>();
+    else
+        k = verify ? kernel_ptr<64, 6, kOffsets, true>() : kernel_ptr<64, 6, kOffsets, false>();
+    return launch(k, a, grid_for(c, count), stream);
+}
+
+}  // namespace
+
+extern "C" {
+
+int mchecksum_gpu_available(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return n > 0 ? 1 : 0;
+}
+
+int mchecksum_gpu_prepare(const char *hash_method) {
+    if (!mchecksum_gpu_available()) return set_err(MCHECKSUM_GPU_ENODEV, "no HIP device%s%d");
+    for (int lg = 0; lg <= CRC_GPU_MAX_LOG2G; lg++) {
+        int width = 0;
+        DevCtx *c = nullptr;
+        const void *pack = nullptr;
+        int rc = prologue(hash_method, lg, &width, &c, &pack);
+        if (rc) return rc;
+    }
+    return MCHECKSUM_GPU_OK;
+}
+
+int mchecksum_gpu_lanes_per_payload(const char *hash_method, size_t len) {
+    int width = 0;
+    if (gpu_model(hash_method, &width) < 0) return -1;
+    return 1 << choose_log2g(len);
+}
+
+int mchecksum_gpu_checksum_fixed(const char *hash_method, const void *dev_base, size_t stride, size_t len,
+                                 size_t count, void *dev_out, void *stream) {
+    if (count && (!dev_base || !dev_out)) return set_err(MCHECKSUM_GPU_EINVAL, "NULL pointer argument%s%d");
+    if (count > 1 && stride < len) return set_err(MCHECKSUM_GPU_EINVAL, "stride smaller than len%s%d");
+    if (!mchecksum_gpu_available()) return set_err(MCHECKSUM_GPU_ENODEV, "no HIP device%s%d");
+    const int lg = choose_log2g(len);
+    int width = 0;
+    DevCtx *c = nullptr;
+    const void *pack = nullptr;
+    int rc = prologue(hash_method, lg, &width, &c, &pack);
+    if (rc) return rc;
+    if (count == 0) return MCHECKSUM_GPU_OK;
+    const uint64_t step = 16ull << lg;
+    const bool aligned = ((uintptr_t)dev_base % 16 == 0) && (stride % 16 == 0 || count == 1) && len >= step &&
+                         (len % step == 0) && !getenv("MCHECKSUM_GPU_FORCE_GENERIC");
+    BatchArgs a{};
+    a.base = (const uint8_t *)dev_base;
+    a.stride = stride;
+    a.len = len;
+    a.count = count;
+    a.out = dev_out;
+    a.pack = pack;
+    kern_t k = width == 32 ? pick_fixed<32>(lg, aligned) : pick_fixed<64>(lg, aligned);
+    const uint64_t ppw = 64u >> lg;
+    return launch(k, a, grid_for(c, (count + ppw - 1) / ppw), stream);
+}
+
+int mchecksum_gpu_checksum_offsets(const char *hash_method, const void *dev_base, const uint64_t *dev_offsets,
+                                   size_t count, void *dev_out, void *stream) {
+    return do_offsets(hash_method, dev_base, dev_offsets, count, dev_out, nullptr, nullptr, nullptr, stream, false);
+}
+
+int mchecksum_gpu_verify_offsets(const char *hash_method, const void *dev_base, const uint64_t *dev_offsets,
+                                 size_t count, const void *dev_expected, uint8_t *dev_status,
+                                 uint32_t *dev_mismatches, void *stream) {
+    return do_offsets(hash_method, dev_base, dev_offsets, count, nullptr, dev_expected, dev_status,
+                      dev_mismatches, stream, true);
+}
+
+const char *mchecksum_gpu_last_error(void) { return t_err; }
+
+}  // extern "C"

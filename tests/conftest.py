@@ -1,0 +1,42 @@
+"""Shared fixtures.  GPU tests are marked @pytest.mark.gpu; everything else
+runs on the CPU (the driver runs `pytest -m "not gpu"` here)."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device)")
+
+
+@pytest.fixture(scope="session")
+def oracle_mod():
+    from oracle import oracle as O
+    O.lib()
+    return O
+
+
+@pytest.fixture(scope="session")
+def product_lib():
+    """libmchecksum.so (built by `make`; the CPU test run builds the
+    host-only objects if hipcc output is absent)."""
+    from mercury_amd import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        subprocess.run(["make", "-s", "-C", ROOT, "all"], check=True)
+    return _lib.load_library()
+
+
+@pytest.fixture(scope="session")
+def gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test selected but no HIP device is visible")
+    from mercury_amd import gpu as G
+    assert G.gpu_available(), "libmchecksum sees no HIP device"
+    return G

@@ -1,0 +1,150 @@
+// kernel_emulator.cpp -- TEST ONLY.  Scalar emulation of the lane-parallel
+// batch-CRC algorithm that mercury_amd/csrc/mchecksum_gpu.hip runs on CDNA4,
+// using the very same host-built table packs (crc_tables.c).  It validates the
+// algebra (window alignment, sub-stream folding, tree combine, tail undo,
+// init handling) on the CPU against the oracle; the GPU parity tests then
+// cover what is GPU-specific (LDS layout, v_perm addressing, shuffles).
+#include "../../mercury_amd/csrc/crc_gpu_layout.h"
+#include "../../oracle/crc_oracle.h"
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+static uint32_t op32(const crc32_gpu_pack_t &pk, int o, uint32_t x) {
+    uint32_t r = 0;
+    for (int h = 0; h < 8; h++) r ^= pk.ops[o][h][(x >> (4 * h)) & 15];
+    return r;
+}
+static uint64_t op64(const crc64_gpu_pack_t &pk, int o, uint64_t x) {
+    uint64_t r = 0;
+    for (int h = 0; h < 16; h++) r ^= pk.ops[o][h][(x >> (4 * h)) & 15];
+    return r;
+}
+
+// Read W/8 bytes at absolute position wa of the virtual address space whose
+// byte at position start..start+len-1 is data[0..len-1]; bytes outside that
+// range are masked to zero; init is XORed into payload bytes [0, W/8).
+template <typename T>
+static T load_word(const uint8_t *data, int64_t start, int64_t len, int64_t wa, T init, bool xinit) {
+    const int nb = sizeof(T);
+    T w = 0;
+    for (int i = 0; i < nb; i++) {
+        int64_t pos = wa + i - start;
+        uint8_t b = 0;
+        if (pos >= 0 && pos < len) b = data[pos];
+        if (xinit && pos >= 0 && pos < nb) b ^= (uint8_t)(init >> (8 * pos));
+        w |= (T)b << (8 * i);
+    }
+    return w;
+}
+
+extern "C" uint32_t emu_crc32(const crc32_gpu_pack_t *pk, const uint8_t *data, int64_t start, int64_t len) {
+    const int log2g = (int)pk->log2g, G = 1 << log2g;
+    const int64_t step = 16LL * G;
+    if (len == 0) return pk->init ^ pk->xorout;
+    int64_t a0 = start & ~15LL, a1 = (start + len + 15) & ~15LL, t = a1 - (start + len);
+    int64_t W = a1 - a0, K = (W + step - 1) / step, v0 = a1 - K * step;
+    std::vector<uint32_t> S(4 * G, 0);
+    bool xinit = len >= 4;
+    for (int64_t k = 0; k < K; k++)
+        for (int l = 0; l < G; l++) {
+            int64_t piece = v0 + k * step + 16 * l;
+            for (int j = 0; j < 4; j++) {
+                uint32_t w = piece >= a0 ? load_word<uint32_t>(data, start, len, piece + 4 * j, pk->init, xinit) : 0;
+                uint32_t x = S[4 * l + j] ^ w;
+                S[4 * l + j] = pk->main[0][x & 255] ^ pk->main[1][(x >> 8) & 255] ^ pk->main[2][(x >> 16) & 255] ^
+                               pk->main[3][x >> 24];
+            }
+        }
+    std::vector<uint32_t> X(G);
+    for (int l = 0; l < G; l++) {
+        uint32_t a = S[4 * l] ^ op32(*pk, 0, S[4 * l + 1]);
+        uint32_t b = S[4 * l + 2] ^ op32(*pk, 0, S[4 * l + 3]);
+        X[l] = a ^ op32(*pk, 1, b);
+    }
+    for (int k = 0; k < log2g; k++) {  // butterfly, as the shuffles do it
+        std::vector<uint32_t> Y(G);
+        for (int l = 0; l < G; l++) {
+            uint32_t other = X[l ^ (1 << k)];
+            bool bit = (l >> k) & 1;
+            uint32_t lo = bit ? other : X[l], hi = bit ? X[l] : other;
+            Y[l] = lo ^ op32(*pk, 2 + k, hi);
+        }
+        X = Y;
+    }
+    uint32_t r = op32(*pk, 2 + log2g + (int)t, X[0]);
+    if (len < 4) r ^= pk->zinit[len];
+    return r ^ pk->xorout;
+}
+
+extern "C" uint64_t emu_crc64(const crc64_gpu_pack_t *pk, const uint8_t *data, int64_t start, int64_t len) {
+    const int log2g = (int)pk->log2g, G = 1 << log2g;
+    const int64_t step = 16LL * G;
+    if (len == 0) return pk->init ^ pk->xorout;
+    int64_t a0 = start & ~15LL, a1 = (start + len + 15) & ~15LL, t = a1 - (start + len);
+    int64_t W = a1 - a0, K = (W + step - 1) / step, v0 = a1 - K * step;
+    std::vector<uint64_t> S(2 * G, 0);
+    bool xinit = len >= 8;
+    for (int64_t k = 0; k < K; k++)
+        for (int l = 0; l < G; l++) {
+            int64_t piece = v0 + k * step + 16 * l;
+            for (int j = 0; j < 2; j++) {
+                uint64_t w = piece >= a0 ? load_word<uint64_t>(data, start, len, piece + 8 * j, pk->init, xinit) : 0;
+                uint64_t x = S[2 * l + j] ^ w, r = 0;
+                for (int p = 0; p < 8; p++)
+                    for (int h = 0; h < 2; h++) r ^= pk->main[2 * p + h][(x >> (8 * p + 4 * h)) & 15];
+                S[2 * l + j] = r;
+            }
+        }
+    std::vector<uint64_t> X(G);
+    for (int l = 0; l < G; l++) X[l] = S[2 * l] ^ op64(*pk, 0, S[2 * l + 1]);
+    for (int k = 0; k < log2g; k++) {
+        std::vector<uint64_t> Y(G);
+        for (int l = 0; l < G; l++) {
+            uint64_t other = X[l ^ (1 << k)];
+            bool bit = (l >> k) & 1;
+            uint64_t lo = bit ? other : X[l], hi = bit ? X[l] : other;
+            Y[l] = lo ^ op64(*pk, 1 + k, hi);
+        }
+        X = Y;
+    }
+    uint64_t r = op64(*pk, 1 + log2g + (int)t, X[0]);
+    if (len < 8) r ^= pk->zinit[len];
+    return r ^ pk->xorout;
+}
+
+#ifdef EMULATOR_MAIN
+int main() {
+    const oracle_model_t *m32 = oracle_model_by_name("crc32c");
+    const oracle_model_t *m64 = oracle_model_by_name("crc64");
+    crc_rmodel_t r32 = {32, 0x82F63B78ULL, 0xFFFFFFFFULL, 0xFFFFFFFFULL};
+    crc_rmodel_t r64 = {64, 0xC96C5795D7870F42ULL, ~0ULL, ~0ULL};
+    std::vector<uint8_t> buf(70000);
+    oracle_fill_splitmix(buf.data(), buf.size(), 0x1234, 0);
+    int fails = 0, n = 0;
+    for (int lg = 0; lg <= 6; lg++) {
+        static crc32_gpu_pack_t p32;
+        static crc64_gpu_pack_t p64;
+        if (crc32_gpu_pack_build(&r32, lg, &p32) || crc64_gpu_pack_build(&r64, lg, &p64)) {
+            printf("pack build failed\n");
+            return 1;
+        }
+        for (int64_t len : {0, 1, 2, 3, 4, 5, 7, 8, 9, 15, 16, 17, 31, 63, 64, 65, 255, 256, 1023, 1024, 1025, 4096, 4097,
+                            65535, 65536})
+            for (int64_t start : {0, 1, 3, 7, 8, 13, 15, 16, 33}) {
+                if (start + len > (int64_t)buf.size()) continue;
+                uint32_t e32 = (uint32_t)oracle_crc_table(m32, buf.data() + start, len);
+                uint64_t e64 = oracle_crc_table(m64, buf.data() + start, len);
+                uint32_t g32 = emu_crc32(&p32, buf.data() + start, start, len);
+                uint64_t g64 = emu_crc64(&p64, buf.data() + start, start, len);
+                n++;
+                if (e32 != g32) { fails++; if (fails < 10) printf("crc32 lg=%d len=%ld start=%ld %08x vs %08x\n", lg, (long)len, (long)start, g32, e32); }
+                if (e64 != g64) { fails++; if (fails < 10) printf("crc64 lg=%d len=%ld start=%ld %016lx vs %016lx\n", lg, (long)len, (long)start, (unsigned long)g64, (unsigned long)e64); }
+            }
+    }
+    printf("%d cases, %d failures\n", n, fails);
+    return fails != 0;
+}
+#endif
