@@ -143,7 +143,7 @@ def main():
             bad += int(got[gi] != want)
         parity = f"bit-exact ({len(idx)} sampled payloads vs oracle)" if bad == 0 else f"MISMATCH {bad}/{len(idx)}"
 
-    total_bytes = payload_bytes * world
+    total_bytes = payload_bytes * world * args.steps  # every rank checksummed its shard once per step
     gib_s = total_bytes / wall_max / 2**30
     out_bytes = count * (4 if G.out_dtype(method) == torch.int32 else 8)
     alg_bytes = payload_bytes + out_bytes + (8 * (count + 1) if layout == "offsets" else 0)

@@ -32,6 +32,7 @@
 #include <mutex>
 
 #include "crc_gpu_layout.h"
+#include "crc_gpu_mask.h"
 #include "mchecksum_gpu.h"
 #include "mchecksum_models.h"
 
@@ -92,16 +93,6 @@ __device__ __forceinline__ uint32_t op32(const uint8_t *lds, uint32_t o, uint32_
 #pragma unroll
     for (int h = 0; h < 8; h++) r ^= lds32(lds, base + h * 64 + (((x >> (4 * h)) & 15u) << 2));
     return r;
-}
-
-__device__ __forceinline__ uint32_t mask32(uint32_t w, int64_t lo, int64_t len, uint32_t init) {
-    if (lo >= len || lo <= -4) return 0;
-    const int sc = lo < 0 ? (int)(-lo) : 0;
-    const int64_t e = lo + 4 - len;
-    const int ec = e > 0 ? (int)e : 0;
-    w &= (0xFFFFFFFFu << (8 * sc)) & (0xFFFFFFFFu >> (8 * ec));
-    if (len >= 4 && lo < 4) w ^= lo >= 0 ? (init << (8 * (int)lo)) : (init >> (8 * (int)(-lo)));
-    return w;
 }
 
 template <int LOG2G>
@@ -207,12 +198,12 @@ __device__ __forceinline__ uint32_t payload32_generic(const uint8_t *lds, const 
             ring[u] = fetch(kk + kRing);
             if (kk < K) {
                 const int64_t pc = r0 + kk * step + lane_off;
-                if (!(pc >= hs + 4 && pc + 16 <= he)) {
+                if (!mck_piece_clean(pc, hs, he, 4)) {
                     const int64_t lo = pc - hs;
-                    v.x = mask32(v.x, lo, ilen, init);
-                    v.y = mask32(v.y, lo + 4, ilen, init);
-                    v.z = mask32(v.z, lo + 8, ilen, init);
-                    v.w = mask32(v.w, lo + 12, ilen, init);
+                    v.x = mck_mask32(v.x, lo, ilen, init);
+                    v.y = mck_mask32(v.y, lo + 4, ilen, init);
+                    v.z = mck_mask32(v.z, lo + 8, ilen, init);
+                    v.w = mck_mask32(v.w, lo + 12, ilen, init);
                 }
                 s0 = f32(lds, s0 ^ v.x, lc0, lc1);
                 s1 = f32(lds, s1 ^ v.y, lc0, lc1);
@@ -326,16 +317,6 @@ __device__ __forceinline__ uint64_t op64(const uint8_t *lds, uint32_t o, uint64_
     return r;
 }
 
-__device__ __forceinline__ uint64_t mask64(uint64_t w, int64_t lo, int64_t len, uint64_t init) {
-    if (lo >= len || lo <= -8) return 0;
-    const int sc = lo < 0 ? (int)(-lo) : 0;
-    const int64_t e = lo + 8 - len;
-    const int ec = e > 0 ? (int)e : 0;
-    w &= (~0ull << (8 * sc)) & (~0ull >> (8 * ec));
-    if (len >= 8 && lo < 8) w ^= lo >= 0 ? (init << (8 * (int)lo)) : (init >> (8 * (int)(-lo)));
-    return w;
-}
-
 template <int LOG2G>
 __device__ __forceinline__ uint64_t combine64(const uint8_t *lds, uint64_t s0, uint64_t s1, uint32_t gl) {
     uint64_t x = s0 ^ op64(lds, 0, s1);
@@ -417,10 +398,10 @@ __device__ __forceinline__ uint64_t payload64_generic(const uint8_t *lds, const 
             if (kk < K) {
                 const int64_t pc = r0 + kk * step + lane_off;
                 uint64_t w0 = (uint64_t)v.y << 32 | v.x, w1 = (uint64_t)v.w << 32 | v.z;
-                if (!(pc >= hs + 8 && pc + 16 <= he)) {
+                if (!mck_piece_clean(pc, hs, he, 8)) {
                     const int64_t lo = pc - hs;
-                    w0 = mask64(w0, lo, ilen, init);
-                    w1 = mask64(w1, lo + 8, ilen, init);
+                    w0 = mck_mask64(w0, lo, ilen, init);
+                    w1 = mck_mask64(w1, lo + 8, ilen, init);
                 }
                 s0 = f64(lds, s0 ^ w0, lc);
                 s1 = f64(lds, s1 ^ w1, lc);

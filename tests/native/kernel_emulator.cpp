@@ -5,6 +5,7 @@
 // init handling) on the CPU against the oracle; the GPU parity tests then
 // cover what is GPU-specific (LDS layout, v_perm addressing, shuffles).
 #include "../../mercury_amd/csrc/crc_gpu_layout.h"
+#include "../../mercury_amd/csrc/crc_gpu_mask.h"
 #include "../../oracle/crc_oracle.h"
 
 #include <cstdio>
@@ -23,37 +24,36 @@ static uint64_t op64(const crc64_gpu_pack_t &pk, int o, uint64_t x) {
     return r;
 }
 
-// Read W/8 bytes at absolute position wa of the virtual address space whose
-// byte at position start..start+len-1 is data[0..len-1]; bytes outside that
-// range are masked to zero; init is XORed into payload bytes [0, W/8).
+// Raw little-endian word at absolute position wa of buf[0, nbuf) (bytes past
+// the buffer read as 0) -- neighbouring payloads' bytes included, exactly as
+// the kernel's aligned loads see them; edge handling is crc_gpu_mask.h's.
 template <typename T>
-static T load_word(const uint8_t *data, int64_t start, int64_t len, int64_t wa, T init, bool xinit) {
-    const int nb = sizeof(T);
+static T raw_word(const uint8_t *buf, int64_t nbuf, int64_t wa) {
     T w = 0;
-    for (int i = 0; i < nb; i++) {
-        int64_t pos = wa + i - start;
-        uint8_t b = 0;
-        if (pos >= 0 && pos < len) b = data[pos];
-        if (xinit && pos >= 0 && pos < nb) b ^= (uint8_t)(init >> (8 * pos));
-        w |= (T)b << (8 * i);
-    }
+    for (int i = 0; i < (int)sizeof(T); i++)
+        if (wa + i >= 0 && wa + i < nbuf) w |= (T)buf[wa + i] << (8 * i);
     return w;
 }
 
-extern "C" uint32_t emu_crc32(const crc32_gpu_pack_t *pk, const uint8_t *data, int64_t start, int64_t len) {
+// CRC of payload buf[start, start+len) as the kernel computes it.
+extern "C" uint32_t emu_crc32(const crc32_gpu_pack_t *pk, const uint8_t *buf, int64_t nbuf, int64_t start,
+                              int64_t len) {
     const int log2g = (int)pk->log2g, G = 1 << log2g;
     const int64_t step = 16LL * G;
-    if (len == 0) return pk->init ^ pk->xorout;
     int64_t a0 = start & ~15LL, a1 = (start + len + 15) & ~15LL, t = a1 - (start + len);
-    int64_t W = a1 - a0, K = (W + step - 1) / step, v0 = a1 - K * step;
+    int64_t W = a1 - a0, K = (W + step - 1) / step, r0 = W - K * step;
+    int64_t hs = start - a0, he = start + len - a0;
     std::vector<uint32_t> S(4 * G, 0);
-    bool xinit = len >= 4;
     for (int64_t k = 0; k < K; k++)
         for (int l = 0; l < G; l++) {
-            int64_t piece = v0 + k * step + 16 * l;
+            int64_t pc = r0 + k * step + 16 * l;
+            uint32_t w[4] = {0, 0, 0, 0};
+            if (pc >= 0)
+                for (int j = 0; j < 4; j++) w[j] = raw_word<uint32_t>(buf, nbuf, a0 + pc + 4 * j);
+            if (!mck_piece_clean(pc, hs, he, 4))
+                for (int j = 0; j < 4; j++) w[j] = mck_mask32(w[j], pc - hs + 4 * j, len, pk->init);
             for (int j = 0; j < 4; j++) {
-                uint32_t w = piece >= a0 ? load_word<uint32_t>(data, start, len, piece + 4 * j, pk->init, xinit) : 0;
-                uint32_t x = S[4 * l + j] ^ w;
+                uint32_t x = S[4 * l + j] ^ w[j];
                 S[4 * l + j] = pk->main[0][x & 255] ^ pk->main[1][(x >> 8) & 255] ^ pk->main[2][(x >> 16) & 255] ^
                                pk->main[3][x >> 24];
             }
@@ -79,20 +79,24 @@ extern "C" uint32_t emu_crc32(const crc32_gpu_pack_t *pk, const uint8_t *data, i
     return r ^ pk->xorout;
 }
 
-extern "C" uint64_t emu_crc64(const crc64_gpu_pack_t *pk, const uint8_t *data, int64_t start, int64_t len) {
+extern "C" uint64_t emu_crc64(const crc64_gpu_pack_t *pk, const uint8_t *buf, int64_t nbuf, int64_t start,
+                              int64_t len) {
     const int log2g = (int)pk->log2g, G = 1 << log2g;
     const int64_t step = 16LL * G;
-    if (len == 0) return pk->init ^ pk->xorout;
     int64_t a0 = start & ~15LL, a1 = (start + len + 15) & ~15LL, t = a1 - (start + len);
-    int64_t W = a1 - a0, K = (W + step - 1) / step, v0 = a1 - K * step;
+    int64_t W = a1 - a0, K = (W + step - 1) / step, r0 = W - K * step;
+    int64_t hs = start - a0, he = start + len - a0;
     std::vector<uint64_t> S(2 * G, 0);
-    bool xinit = len >= 8;
     for (int64_t k = 0; k < K; k++)
         for (int l = 0; l < G; l++) {
-            int64_t piece = v0 + k * step + 16 * l;
+            int64_t pc = r0 + k * step + 16 * l;
+            uint64_t w[2] = {0, 0};
+            if (pc >= 0)
+                for (int j = 0; j < 2; j++) w[j] = raw_word<uint64_t>(buf, nbuf, a0 + pc + 8 * j);
+            if (!mck_piece_clean(pc, hs, he, 8))
+                for (int j = 0; j < 2; j++) w[j] = mck_mask64(w[j], pc - hs + 8 * j, len, pk->init);
             for (int j = 0; j < 2; j++) {
-                uint64_t w = piece >= a0 ? load_word<uint64_t>(data, start, len, piece + 8 * j, pk->init, xinit) : 0;
-                uint64_t x = S[2 * l + j] ^ w, r = 0;
+                uint64_t x = S[2 * l + j] ^ w[j], r = 0;
                 for (int p = 0; p < 8; p++)
                     for (int h = 0; h < 2; h++) r ^= pk->main[2 * p + h][(x >> (8 * p + 4 * h)) & 15];
                 S[2 * l + j] = r;
@@ -133,12 +137,12 @@ int main() {
         }
         for (int64_t len : {0, 1, 2, 3, 4, 5, 7, 8, 9, 15, 16, 17, 31, 63, 64, 65, 255, 256, 1023, 1024, 1025, 4096, 4097,
                             65535, 65536})
-            for (int64_t start : {0, 1, 3, 7, 8, 13, 15, 16, 33}) {
+            for (int64_t start : {0, 1, 2, 3, 4, 5, 7, 8, 11, 12, 13, 15, 16, 33}) {
                 if (start + len > (int64_t)buf.size()) continue;
                 uint32_t e32 = (uint32_t)oracle_crc_table(m32, buf.data() + start, len);
                 uint64_t e64 = oracle_crc_table(m64, buf.data() + start, len);
-                uint32_t g32 = emu_crc32(&p32, buf.data() + start, start, len);
-                uint64_t g64 = emu_crc64(&p64, buf.data() + start, start, len);
+                uint32_t g32 = emu_crc32(&p32, buf.data(), (int64_t)buf.size(), start, len);
+                uint64_t g64 = emu_crc64(&p64, buf.data(), (int64_t)buf.size(), start, len);
                 n++;
                 if (e32 != g32) { fails++; if (fails < 10) printf("crc32 lg=%d len=%ld start=%ld %08x vs %08x\n", lg, (long)len, (long)start, g32, e32); }
                 if (e64 != g64) { fails++; if (fails < 10) printf("crc64 lg=%d len=%ld start=%ld %016lx vs %016lx\n", lg, (long)len, (long)start, (unsigned long)g64, (unsigned long)e64); }
