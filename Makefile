@@ -57,3 +57,16 @@ clean:
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean cpu asm
+
+# A/B variants of the batch kernels (tools/ab_variants.py).  Each is a full
+# libmchecksum built with different tuning macros.
+VARIANTS := base:-DMCK_RING=4 ring2:-DMCK_RING=2 ring8:-DMCK_RING=8 \
+            blk512:-DMCK_BLOCK=512
+variants: $(COBJS) | $(BUILD)
+	mkdir -p $(BUILD)/variants
+	@for v in $(VARIANTS); do n=$${v%%:*}; f=$$(echo $${v#*:} | tr , " "); \
+	  echo "variant $$n: $$f"; \
+	  $(HIPCC) $(HIPFLAGS) $$f $(INC) -c $(CSRC)/mchecksum_gpu.hip -o $(BUILD)/variants/gpu_$$n.o && \
+	  $(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $(BUILD)/variants/libmchecksum_$$n.so $(COBJS) $(BUILD)/variants/gpu_$$n.o -lpthread || exit 1; \
+	done
+.PHONY: variants

@@ -38,9 +38,17 @@
 
 namespace {
 
-constexpr int kBlock = 1024;  // 16 waves: 4 per SIMD
+// Build-time tuning knobs (A/B builds: tools/ab_variants.py); defaults are
+// the measured best.
+#ifndef MCK_BLOCK
+#define MCK_BLOCK 1024
+#endif
+#ifndef MCK_RING
+#define MCK_RING 4
+#endif
+constexpr int kBlock = MCK_BLOCK;  // 1024 = 16 waves: 4 per SIMD
 constexpr int kWavesPerBlock = kBlock / 64;
-constexpr int kRing = 4;  // dwordx4 pieces in flight per lane
+constexpr int kRing = MCK_RING;  // dwordx4 pieces in flight per lane
 
 // CRC-32C LDS map: [0,128K) main byte tables x32 copies; then op nibble tables.
 constexpr uint32_t kL32Main = 131072;
@@ -62,11 +70,21 @@ struct BatchArgs {
     const void *pack;
 };
 
-#ifdef MCHECKSUM_NT_LOADS
-__device__ __forceinline__ uint4 ld16(const uint4 *p) { return __builtin_nontemporal_load(p); }
-#else
-__device__ __forceinline__ uint4 ld16(const uint4 *p) { return *p; }
-#endif
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+
+// Payload bytes are read exactly once.  Non-temporal loads keep a batch far
+// larger than the 256 MiB Infinity Cache from churning the caches: +13% on the
+// 4 GiB headline batch (profiles/r01/ab1.log); a small batch replayed
+// back to back is faster with the default policy (it partly hits the cache).
+template <bool NT>
+__device__ __forceinline__ uint4 ld16(const uint4 *p) {
+    if constexpr (NT) {
+        const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t *>(p));
+        return make_uint4(v.x, v.y, v.z, v.w);
+    } else {
+        return *p;
+    }
+}
 
 __device__ __forceinline__ uint32_t lds32(const uint8_t *lds, uint32_t a) {
     return *reinterpret_cast<const uint32_t *>(lds + a);
@@ -124,7 +142,7 @@ __device__ void fill_lds32(uint8_t *lds, const crc32_gpu_pack_t *pk) {
 
 // Aligned fixed-size payload: base 16-B aligned, len = K * 16G, no masking,
 // no pad bytes (tail op is the identity and is skipped).
-template <int LOG2G>
+template <int LOG2G, bool NT>
 __device__ __forceinline__ uint32_t payload32_aligned(const uint8_t *lds, const uint8_t *p, uint64_t K, uint32_t gl,
                                                       uint32_t lc0, uint32_t lc1, uint32_t init) {
     constexpr int G = 1 << LOG2G;
@@ -132,13 +150,13 @@ __device__ __forceinline__ uint32_t payload32_aligned(const uint8_t *lds, const 
     uint32_t s0 = gl == 0 ? init : 0u, s1 = 0, s2 = 0, s3 = 0;
     uint4 ring[kRing];
 #pragma unroll
-    for (int u = 0; u < kRing; u++) ring[u] = (uint64_t)u < K ? ld16(src + (uint64_t)u * G) : make_uint4(0, 0, 0, 0);
+    for (int u = 0; u < kRing; u++) ring[u] = (uint64_t)u < K ? ld16<NT>(src + (uint64_t)u * G) : make_uint4(0, 0, 0, 0);
     for (uint64_t k = 0; k < K; k += kRing) {
 #pragma unroll
         for (int u = 0; u < kRing; u++) {
             const uint4 v = ring[u];
             const uint64_t kn = k + u + kRing;
-            if (kn < K) ring[u] = ld16(src + kn * G);
+            if (kn < K) ring[u] = ld16<NT>(src + kn * G);
             if (k + u < K) {
                 s0 = f32(lds, s0 ^ v.x, lc0, lc1);
                 s1 = f32(lds, s1 ^ v.y, lc0, lc1);
@@ -162,7 +180,7 @@ __device__ __forceinline__ T wave_max(T v) {
 
 // Any alignment, any length (0 included).  Per-lane window; the wave loops to
 // the largest step count of its groups.
-template <int LOG2G>
+template <int LOG2G, bool NT>
 __device__ __forceinline__ uint32_t payload32_generic(const uint8_t *lds, const crc32_gpu_pack_t *pk,
                                                       const uint8_t *p, uint64_t len, uint32_t gl, uint32_t lc0,
                                                       uint32_t lc1) {
@@ -182,7 +200,7 @@ __device__ __forceinline__ uint32_t payload32_generic(const uint8_t *lds, const 
     auto fetch = [&](int64_t k) -> uint4 {
         const int64_t pc = r0 + k * step + lane_off;
         uint4 v = make_uint4(0, 0, 0, 0);
-        if (k < K && pc >= 0) v = ld16(reinterpret_cast<const uint4 *>(a0 + (uint64_t)pc));
+        if (k < K && pc >= 0) v = ld16<NT>(reinterpret_cast<const uint4 *>(a0 + (uint64_t)pc));
         return v;
     };
 
@@ -251,7 +269,7 @@ __device__ __forceinline__ void emit(const BatchArgs &a, uint64_t p, T v) {
     }
 }
 
-template <int LOG2G, int MODE, bool VERIFY>
+template <int LOG2G, int MODE, bool VERIFY, bool NT>
 __global__ __launch_bounds__(kBlock, 1) void crc32c_batch_kernel(BatchArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kL32Bytes];
     const crc32_gpu_pack_t *pk = reinterpret_cast<const crc32_gpu_pack_t *>(a.pack);
@@ -271,7 +289,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_batch_kernel(BatchArgs a) {
         wave_range(a.offsets, a.count, wave, nw, &first, &last);
         for (uint64_t p = first; p < last; p++) {
             const uint64_t o = a.offsets[p];
-            const uint32_t x = payload32_generic<LOG2G>(lds, pk, a.base + o, a.offsets[p + 1] - o, gl, lc0, lc1);
+            const uint32_t x = payload32_generic<LOG2G, NT>(lds, pk, a.base + o, a.offsets[p + 1] - o, gl, lc0, lc1);
             if (gl == 0) emit<uint32_t, VERIFY>(a, p, x ^ xorout);
         }
         return;
@@ -282,9 +300,9 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_batch_kernel(BatchArgs a) {
         const uint64_t pc = act ? p : a.count - 1;
         uint32_t x;
         if (MODE == kFixedAligned)
-            x = payload32_aligned<LOG2G>(lds, a.base + pc * a.stride, a.len >> (4 + LOG2G), gl, lc0, lc1, pk->init);
+            x = payload32_aligned<LOG2G, NT>(lds, a.base + pc * a.stride, a.len >> (4 + LOG2G), gl, lc0, lc1, pk->init);
         else
-            x = payload32_generic<LOG2G>(lds, pk, a.base + pc * a.stride, a.len, gl, lc0, lc1);
+            x = payload32_generic<LOG2G, NT>(lds, pk, a.base + pc * a.stride, a.len, gl, lc0, lc1);
         if (act && gl == 0) emit<uint32_t, VERIFY>(a, p, x ^ xorout);
     }
 }
@@ -338,7 +356,7 @@ __device__ void fill_lds64(uint8_t *lds, const crc64_gpu_pack_t *pk) {
     for (uint32_t d = threadIdx.x; d < nops; d += kBlock) l[kL64Main / 8 + d] = ops[d];
 }
 
-template <int LOG2G>
+template <int LOG2G, bool NT>
 __device__ __forceinline__ uint64_t payload64_aligned(const uint8_t *lds, const uint8_t *p, uint64_t K, uint32_t gl,
                                                       uint32_t lc, uint64_t init) {
     constexpr int G = 1 << LOG2G;
@@ -346,13 +364,13 @@ __device__ __forceinline__ uint64_t payload64_aligned(const uint8_t *lds, const 
     uint64_t s0 = gl == 0 ? init : 0ull, s1 = 0;
     uint4 ring[kRing];
 #pragma unroll
-    for (int u = 0; u < kRing; u++) ring[u] = (uint64_t)u < K ? ld16(src + (uint64_t)u * G) : make_uint4(0, 0, 0, 0);
+    for (int u = 0; u < kRing; u++) ring[u] = (uint64_t)u < K ? ld16<NT>(src + (uint64_t)u * G) : make_uint4(0, 0, 0, 0);
     for (uint64_t k = 0; k < K; k += kRing) {
 #pragma unroll
         for (int u = 0; u < kRing; u++) {
             const uint4 v = ring[u];
             const uint64_t kn = k + u + kRing;
-            if (kn < K) ring[u] = ld16(src + kn * G);
+            if (kn < K) ring[u] = ld16<NT>(src + kn * G);
             if (k + u < K) {
                 s0 = f64(lds, s0 ^ ((uint64_t)v.y << 32 | v.x), lc);
                 s1 = f64(lds, s1 ^ ((uint64_t)v.w << 32 | v.z), lc);
@@ -362,7 +380,7 @@ __device__ __forceinline__ uint64_t payload64_aligned(const uint8_t *lds, const 
     return combine64<LOG2G>(lds, s0, s1, gl);
 }
 
-template <int LOG2G>
+template <int LOG2G, bool NT>
 __device__ __forceinline__ uint64_t payload64_generic(const uint8_t *lds, const crc64_gpu_pack_t *pk,
                                                       const uint8_t *p, uint64_t len, uint32_t gl, uint32_t lc) {
     constexpr int G = 1 << LOG2G;
@@ -381,7 +399,7 @@ __device__ __forceinline__ uint64_t payload64_generic(const uint8_t *lds, const 
     auto fetch = [&](int64_t k) -> uint4 {
         const int64_t pc = r0 + k * step + lane_off;
         uint4 v = make_uint4(0, 0, 0, 0);
-        if (k < K && pc >= 0) v = ld16(reinterpret_cast<const uint4 *>(a0 + (uint64_t)pc));
+        if (k < K && pc >= 0) v = ld16<NT>(reinterpret_cast<const uint4 *>(a0 + (uint64_t)pc));
         return v;
     };
 
@@ -414,7 +432,7 @@ __device__ __forceinline__ uint64_t payload64_generic(const uint8_t *lds, const 
     return x;
 }
 
-template <int LOG2G, int MODE, bool VERIFY>
+template <int LOG2G, int MODE, bool VERIFY, bool NT>
 __global__ __launch_bounds__(kBlock, 1) void crc64_batch_kernel(BatchArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kL64Bytes];
     const crc64_gpu_pack_t *pk = reinterpret_cast<const crc64_gpu_pack_t *>(a.pack);
@@ -434,7 +452,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc64_batch_kernel(BatchArgs a) {
         wave_range(a.offsets, a.count, wave, nw, &first, &last);
         for (uint64_t p = first; p < last; p++) {
             const uint64_t o = a.offsets[p];
-            const uint64_t x = payload64_generic<LOG2G>(lds, pk, a.base + o, a.offsets[p + 1] - o, gl, lc);
+            const uint64_t x = payload64_generic<LOG2G, NT>(lds, pk, a.base + o, a.offsets[p + 1] - o, gl, lc);
             if (gl == 0) emit<uint64_t, VERIFY>(a, p, x ^ xorout);
         }
         return;
@@ -445,9 +463,9 @@ __global__ __launch_bounds__(kBlock, 1) void crc64_batch_kernel(BatchArgs a) {
         const uint64_t pc = act ? p : a.count - 1;
         uint64_t x;
         if (MODE == kFixedAligned)
-            x = payload64_aligned<LOG2G>(lds, a.base + pc * a.stride, a.len >> (4 + LOG2G), gl, lc, pk->init);
+            x = payload64_aligned<LOG2G, NT>(lds, a.base + pc * a.stride, a.len >> (4 + LOG2G), gl, lc, pk->init);
         else
-            x = payload64_generic<LOG2G>(lds, pk, a.base + pc * a.stride, a.len, gl, lc);
+            x = payload64_generic<LOG2G, NT>(lds, pk, a.base + pc * a.stride, a.len, gl, lc);
         if (act && gl == 0) emit<uint64_t, VERIFY>(a, p, x ^ xorout);
     }
 }
@@ -560,23 +578,37 @@ int choose_log2g(size_t len) {
 
 typedef void (*kern_t)(BatchArgs);
 
-template <int W, int LOG2G, int MODE, bool VERIFY>
+template <int W, int LOG2G, int MODE, bool VERIFY, bool NT = false>
 kern_t kernel_ptr() {
-    if constexpr (W == 32) return crc32c_batch_kernel<LOG2G, MODE, VERIFY>;
-    else return crc64_batch_kernel<LOG2G, MODE, VERIFY>;
+    if constexpr (W == 32) return crc32c_batch_kernel<LOG2G, MODE, VERIFY, NT>;
+    else return crc64_batch_kernel<LOG2G, MODE, VERIFY, NT>;
+}
+
+template <int W, int LOG2G>
+kern_t pick_fixed_lg(bool aligned, bool nt) {
+    if (!aligned) return kernel_ptr<W, LOG2G, kFixedGeneric, false>();
+    return nt ? kernel_ptr<W, LOG2G, kFixedAligned, false, true>() : kernel_ptr<W, LOG2G, kFixedAligned, false>();
 }
 
 template <int W>
-kern_t pick_fixed(int log2g, bool aligned) {
+kern_t pick_fixed(int log2g, bool aligned, bool nt) {
     switch (log2g) {
-        case 0: return aligned ? kernel_ptr<W, 0, kFixedAligned, false>() : kernel_ptr<W, 0, kFixedGeneric, false>();
-        case 1: return aligned ? kernel_ptr<W, 1, kFixedAligned, false>() : kernel_ptr<W, 1, kFixedGeneric, false>();
-        case 2: return aligned ? kernel_ptr<W, 2, kFixedAligned, false>() : kernel_ptr<W, 2, kFixedGeneric, false>();
-        case 3: return aligned ? kernel_ptr<W, 3, kFixedAligned, false>() : kernel_ptr<W, 3, kFixedGeneric, false>();
-        case 4: return aligned ? kernel_ptr<W, 4, kFixedAligned, false>() : kernel_ptr<W, 4, kFixedGeneric, false>();
-        case 5: return aligned ? kernel_ptr<W, 5, kFixedAligned, false>() : kernel_ptr<W, 5, kFixedGeneric, false>();
-        default: return aligned ? kernel_ptr<W, 6, kFixedAligned, false>() : kernel_ptr<W, 6, kFixedGeneric, false>();
+        case 0: return pick_fixed_lg<W, 0>(aligned, nt);
+        case 1: return pick_fixed_lg<W, 1>(aligned, nt);
+        case 2: return pick_fixed_lg<W, 2>(aligned, nt);
+        case 3: return pick_fixed_lg<W, 3>(aligned, nt);
+        case 4: return pick_fixed_lg<W, 4>(aligned, nt);
+        case 5: return pick_fixed_lg<W, 5>(aligned, nt);
+        default: return pick_fixed_lg<W, 6>(aligned, nt);
     }
+}
+
+// Non-temporal payload loads when the batch is far larger than the 256 MiB
+// Infinity Cache (MCHECKSUM_GPU_NT=0/1 overrides).
+bool use_nt(uint64_t batch_bytes) {
+    const char *env = getenv("MCHECKSUM_GPU_NT");
+    if (env && env[0]) return env[0] == '1';
+    return batch_bytes >= (512ull << 20);
 }
 
 int launch(kern_t k, const BatchArgs &a, unsigned blocks, void *stream) {
@@ -623,10 +655,15 @@ int do_offsets(const char *method, const void *base, const uint64_t *offsets, si
     a.mismatches = mism;
     a.pack = pack;
     kern_t k;
+    // The offsets table stays on the device, so size the batch by its count:
+    // 8192+ payloads of the C4 mix are ~270 MB and up.
+    const bool nt = use_nt(count >= 8192 ? (1ull << 40) : 0);
     if (width == 32)
-        k = verify ? kernel_ptr<32, 6, kOffsets, true>() : kernel_ptr<32, 6, kOffsets, false>();
+        k = verify ? (nt ? kernel_ptr<32, 6, kOffsets, true, true>() : kernel_ptr<32, 6, kOffsets, true>())
+                   : (nt ? kernel_ptr<32, 6, kOffsets, false, true>() : kernel_ptr<32, 6, kOffsets, false>());
     else
-        k = verify ? kernel_ptr<64, 6, kOffsets, true>() : kernel_ptr<64, 6, kOffsets, false>();
+        k = verify ? (nt ? kernel_ptr<64, 6, kOffsets, true, true>() : kernel_ptr<64, 6, kOffsets, true>())
+                   : (nt ? kernel_ptr<64, 6, kOffsets, false, true>() : kernel_ptr<64, 6, kOffsets, false>());
     return launch(k, a, grid_for(c, count), stream);
 }
 
@@ -683,7 +720,8 @@ int mchecksum_gpu_checksum_fixed(const char *hash_method, const void *dev_base, 
     a.count = count;
     a.out = dev_out;
     a.pack = pack;
-    kern_t k = width == 32 ? pick_fixed<32>(lg, aligned) : pick_fixed<64>(lg, aligned);
+    const bool nt = use_nt((uint64_t)len * count);
+    kern_t k = width == 32 ? pick_fixed<32>(lg, aligned, nt) : pick_fixed<64>(lg, aligned, nt);
     const uint64_t ppw = 64u >> lg;
     return launch(k, a, grid_for(c, (count + ppw - 1) / ppw), stream);
 }

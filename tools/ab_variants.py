@@ -1,0 +1,112 @@
+#!/usr/bin/env python3
+"""A/B the batch-kernel variants built by `make variants` in ONE process,
+interleaved round by round (cdna_hip_programming.md sec. 5.4 rule 24).
+
+Every variant must produce the same CRCs as the default library; the script
+prints per-variant median/min kernel time and achieved HBM GB/s.
+"""
+import argparse
+import ctypes
+import glob
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from mercury_amd import gpu as G  # noqa: E402
+
+SHAPES = {
+    "metric": ("crc32c", 65536, 65536, 0x4D43310000000005),
+    "c2": ("crc32c", 65536, 4096, 0x4D43310000000002),
+    "c3": ("crc64", 8192, 1 << 20, 0x4D43310000000003),
+}
+
+
+def load(path):
+    L = ctypes.CDLL(path)
+    c = ctypes
+    L.mchecksum_gpu_prepare.argtypes = [c.c_char_p]
+    L.mchecksum_gpu_checksum_fixed.argtypes = [c.c_char_p, c.c_void_p, c.c_size_t, c.c_size_t, c.c_size_t,
+                                               c.c_void_p, c.c_void_p]
+    L.mchecksum_gpu_checksum_offsets.argtypes = [c.c_char_p, c.c_void_p, c.c_void_p, c.c_size_t, c.c_void_p,
+                                                 c.c_void_p]
+    return L
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="metric")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--variants", nargs="*", default=None)
+    ap.add_argument("--env", nargs="*", default=[],
+                    help="extra pseudo-variants of the default library: NAME=VAR=VALUE (env set around its calls)")
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+
+    paths = sorted(glob.glob(os.path.join(ROOT, "build", "variants", "libmchecksum_*.so")))
+    if args.variants:
+        paths = [p for p in paths if os.path.basename(p)[len("libmchecksum_"):-3] in args.variants]
+    names = [os.path.basename(p)[len("libmchecksum_"):-3] for p in paths]
+    libs = [load(p) for p in paths]
+    envs = [None] * len(libs)
+    for spec in args.env:
+        nm, var, val = spec.split("=", 2)
+        names.append(nm)
+        libs.append(load(os.path.join(ROOT, "mercury_amd", "lib", "libmchecksum.so")))
+        envs.append((var, val))
+
+    results = {}
+    configs = args.config.split(",")
+    for cfg in configs:
+        method, count, length, seed = SHAPES[cfg]
+        data = torch.empty(count * length + 64, dtype=torch.uint8, device="cuda")
+        G.fill_splitmix(data, seed)
+        ref = G.checksum_fixed(method, data, length, count=count)
+        torch.cuda.synchronize()
+        stream = torch.cuda.current_stream()
+        h = stream.cuda_stream
+        outs = [torch.empty_like(ref) for _ in libs]
+        for L in libs:
+            assert L.mchecksum_gpu_prepare(method.encode()) == 0
+        times = {n: [] for n in names}
+        for r in range(args.rounds + 1):
+            for n, L, o, e in zip(names, libs, outs, envs):
+                if e:
+                    os.environ[e[0]] = e[1]
+                evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                       for _ in range(args.iters)]
+                for a, b in evs:
+                    a.record(stream)
+                    rc = L.mchecksum_gpu_checksum_fixed(method.encode(), data.data_ptr(), length, length, count,
+                                                        o.data_ptr(), h)
+                    b.record(stream)
+                    assert rc == 0
+                torch.cuda.synchronize()
+                if e:
+                    del os.environ[e[0]]
+                if r > 0:  # round 0 = warm-up
+                    times[n] += [a.elapsed_time(b) for a, b in evs]
+        for n, o in zip(names, outs):
+            assert torch.equal(o, ref), f"variant {n} differs from the default library"
+        nbytes = count * length
+        res = {}
+        for n in names:
+            t = np.array(times[n])
+            res[n] = {"median_ms": float(np.median(t)), "min_ms": float(t.min()),
+                      "GBs_median": nbytes / (np.median(t) * 1e-3) / 1e9, "GBs_best": nbytes / (t.min() * 1e-3) / 1e9}
+            print(f"{cfg:7s} {n:10s} median {res[n]['median_ms']:.4f} ms  min {res[n]['min_ms']:.4f} ms  "
+                  f"{res[n]['GBs_median']:.0f} GB/s (best {res[n]['GBs_best']:.0f})", flush=True)
+        results[cfg] = res
+        del data
+        torch.cuda.empty_cache()
+    if args.out:
+        json.dump(results, open(args.out, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
