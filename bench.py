@@ -67,6 +67,7 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
 
     from mercury_amd import gpu as G
+    from mercury_amd.shard import fixed_shard
 
     method, count, length, seed, layout = CONFIGS[args.config]
     stream = torch.cuda.current_stream()
@@ -76,7 +77,8 @@ def main():
     if layout == "fixed":
         nbytes = count * length
         data = torch.empty(nbytes + 64, dtype=torch.uint8, device=dev)
-        first_word = (rank * nbytes) // 8  # shard r = payloads [r*count, (r+1)*count)
+        first_payload, _ = fixed_shard(rank, world, count * world)  # shard r = payloads [r*count, (r+1)*count)
+        first_word = first_payload * length // 8
         G.fill_splitmix(data, seed, first_word=first_word)
         offsets_dev = offsets_host = None
         payload_bytes = nbytes

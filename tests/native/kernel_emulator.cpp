@@ -152,3 +152,19 @@ int main() {
     return fails != 0;
 }
 #endif
+
+// ctypes entry points for tests/test_emulator.py
+extern "C" void *emu_pack32(int log2g) {
+    auto *p = new crc32_gpu_pack_t;
+    crc_rmodel_t r = {32, 0x82F63B78ULL, 0xFFFFFFFFULL, 0xFFFFFFFFULL};
+    if (crc32_gpu_pack_build(&r, log2g, p)) { delete p; return nullptr; }
+    return p;
+}
+extern "C" void *emu_pack64(int log2g) {
+    auto *p = new crc64_gpu_pack_t;
+    crc_rmodel_t r = {64, 0xC96C5795D7870F42ULL, ~0ULL, ~0ULL};
+    if (crc64_gpu_pack_build(&r, log2g, p)) { delete p; return nullptr; }
+    return p;
+}
+extern "C" void emu_pack_free32(void *p) { delete (crc32_gpu_pack_t *)p; }
+extern "C" void emu_pack_free64(void *p) { delete (crc64_gpu_pack_t *)p; }
