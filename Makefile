@@ -34,6 +34,7 @@ $(BUILD)/bench_datagen.o: $(CSRC)/bench_datagen.hip | $(BUILD)
 
 $(LIB): $(COBJS) $(GOBJS) | $(LIBDIR)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^ -lpthread -Wl,-soname,libmchecksum.so.2
+	ln -sf libmchecksum.so $(LIBDIR)/libmchecksum.so.2
 
 $(BENCHLIB): $(BUILD)/bench_datagen.o | $(LIBDIR)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^
