@@ -61,8 +61,7 @@ clean:
 
 # A/B variants of the batch kernels (tools/ab_variants.py).  Each is a full
 # libmchecksum built with different tuning macros.
-VARIANTS := base:-DMCK_RING=4 ring2:-DMCK_RING=2 ring8:-DMCK_RING=8 \
-            blk512:-DMCK_BLOCK=512
+VARIANTS := base:-DMCK_RING=4 nobitop3:-DMCK_BITOP3=0 ring6:-DMCK_RING=6 ring8:-DMCK_RING=8
 variants: $(COBJS) | $(BUILD)
 	mkdir -p $(BUILD)/variants
 	@for v in $(VARIANTS); do n=$${v%%:*}; f=$$(echo $${v#*:} | tr , " "); \

@@ -42,12 +42,14 @@ CONFIGS = {
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--config", default="metric", choices=sorted(CONFIGS))
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=1.5, help="wall budget of the CPU baseline sample")
     p.add_argument("--parity-samples", type=int, default=64)
+    p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                   help="nccl = RCCL (default); gloo only to rehearse the multi-rank flow on one GPU")
     return p.parse_args()
 
 
@@ -60,8 +62,11 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        torch.cuda.set_device(local % torch.cuda.device_count())
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -114,7 +119,8 @@ def main():
     wall = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
 
-    t = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev)
+    coll_dev = dev if args.backend == "nccl" else torch.device("cpu")
+    t = torch.tensor([wall, kern_ms], dtype=torch.float64, device=coll_dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall_max, kern_ms_max = float(t[0]), float(t[1])
@@ -122,8 +128,9 @@ def main():
     # ---- parity on the gathered result (outside the timed region) --------
     crcs = out
     if world > 1:
-        gathered = [torch.empty_like(out) for _ in range(world)]
-        dist.all_gather(gathered, out)
+        mine = out.to(coll_dev)
+        gathered = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(gathered, mine)
         crcs = torch.cat(gathered)
     parity = "unchecked"
     if rank == 0:

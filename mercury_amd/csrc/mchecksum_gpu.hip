@@ -46,6 +46,9 @@ namespace {
 #ifndef MCK_RING
 #define MCK_RING 4
 #endif
+#ifndef MCK_BITOP3
+#define MCK_BITOP3 1
+#endif
 constexpr int kBlock = MCK_BLOCK;  // 1024 = 16 waves: 4 per SIMD
 constexpr int kWavesPerBlock = kBlock / 64;
 constexpr int kRing = MCK_RING;  // dwordx4 pieces in flight per lane
@@ -95,22 +98,37 @@ __device__ __forceinline__ uint64_t lds64(const uint8_t *lds, uint32_t a) {
 
 // ---------------------------------------------------------------- CRC-32C --
 
-// s' = Z^(16G)(x): main[p][byte_p(x)], tables p=0,1 in LDS region 0 (lc0),
-// p=2,3 in region 1 (lc1 has +64 KiB in its byte 2); odd p at +128 B.
-__device__ __forceinline__ uint32_t f32(const uint8_t *lds, uint32_t x, uint32_t lc0, uint32_t lc1) {
+// a ^ b ^ c in one VALU op: gfx950's v_bitop3_b32 with truth table 0x96
+// (there is no v_xor3_b32 on CDNA; hipcc does not form bitop3 from ^ chains).
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+#if MCK_BITOP3
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+#else
+    return a ^ b ^ c;
+#endif
+}
+
+// Z^(16G)(x): main[p][byte_p(x)], tables p=0,1 in LDS region 0 (lc0), p=2,3
+// in region 1 (lc1 has +64 KiB in its byte 2); odd p at +128 B.  One step of
+// a sub-stream costs 4 v_perm + 2 v_bitop3 (+1 XOR with the data word) per
+// 4 bytes.  (Folding the next word into this XOR tree instead -- a look-ahead
+// pipeline -- measured 7% slower on the headline batch, profiles/r01/ab3.log.)
+__device__ __forceinline__ uint32_t f32s(const uint8_t *lds, uint32_t x, uint32_t lc0, uint32_t lc1) {
     const uint32_t a0 = __builtin_amdgcn_perm(x, lc0, 0x0C020400u);
     const uint32_t a1 = __builtin_amdgcn_perm(x, lc0, 0x0C020500u);
     const uint32_t a2 = __builtin_amdgcn_perm(x, lc1, 0x0C020600u);
     const uint32_t a3 = __builtin_amdgcn_perm(x, lc1, 0x0C020700u);
-    return lds32(lds, a0) ^ lds32(lds, a1 + 128) ^ lds32(lds, a2) ^ lds32(lds, a3 + 128);
+    return xor3(lds32(lds, a0), lds32(lds, a1 + 128), lds32(lds, a2)) ^ lds32(lds, a3 + 128);
 }
 
 __device__ __forceinline__ uint32_t op32(const uint8_t *lds, uint32_t o, uint32_t x) {
     const uint32_t base = kL32Main + o * 512;
-    uint32_t r = 0;
+    uint32_t t[8];
 #pragma unroll
-    for (int h = 0; h < 8; h++) r ^= lds32(lds, base + h * 64 + (((x >> (4 * h)) & 15u) << 2));
-    return r;
+    for (int h = 0; h < 8; h++) t[h] = lds32(lds, base + h * 64 + (((x >> (4 * h)) & 15u) << 2));
+    return xor3(xor3(t[0], t[1], t[2]), xor3(t[3], t[4], t[5]), t[6] ^ t[7]);
 }
 
 template <int LOG2G>
@@ -140,6 +158,8 @@ __device__ void fill_lds32(uint8_t *lds, const crc32_gpu_pack_t *pk) {
     for (uint32_t d = threadIdx.x; d < nops; d += kBlock) l[kL32Main / 4 + d] = ops[d];
 }
 
+// Ring slot j % kRing holds the piece of step j, loaded kRing steps ahead.
+//
 // Aligned fixed-size payload: base 16-B aligned, len = K * 16G, no masking,
 // no pad bytes (tail op is the identity and is skipped).
 template <int LOG2G, bool NT>
@@ -147,10 +167,10 @@ __device__ __forceinline__ uint32_t payload32_aligned(const uint8_t *lds, const 
                                                       uint32_t lc0, uint32_t lc1, uint32_t init) {
     constexpr int G = 1 << LOG2G;
     const uint4 *src = reinterpret_cast<const uint4 *>(p) + gl;
-    uint32_t s0 = gl == 0 ? init : 0u, s1 = 0, s2 = 0, s3 = 0;
     uint4 ring[kRing];
 #pragma unroll
     for (int u = 0; u < kRing; u++) ring[u] = (uint64_t)u < K ? ld16<NT>(src + (uint64_t)u * G) : make_uint4(0, 0, 0, 0);
+    uint32_t x0 = gl == 0 ? init : 0u, x1 = 0, x2 = 0, x3 = 0;
     for (uint64_t k = 0; k < K; k += kRing) {
 #pragma unroll
         for (int u = 0; u < kRing; u++) {
@@ -158,14 +178,14 @@ __device__ __forceinline__ uint32_t payload32_aligned(const uint8_t *lds, const 
             const uint64_t kn = k + u + kRing;
             if (kn < K) ring[u] = ld16<NT>(src + kn * G);
             if (k + u < K) {
-                s0 = f32(lds, s0 ^ v.x, lc0, lc1);
-                s1 = f32(lds, s1 ^ v.y, lc0, lc1);
-                s2 = f32(lds, s2 ^ v.z, lc0, lc1);
-                s3 = f32(lds, s3 ^ v.w, lc0, lc1);
+                x0 = f32s(lds, x0 ^ v.x, lc0, lc1);
+                x1 = f32s(lds, x1 ^ v.y, lc0, lc1);
+                x2 = f32s(lds, x2 ^ v.z, lc0, lc1);
+                x3 = f32s(lds, x3 ^ v.w, lc0, lc1);
             }
         }
     }
-    return combine32<LOG2G>(lds, s0, s1, s2, s3, gl);
+    return combine32<LOG2G>(lds, x0, x1, x2, x3, gl);
 }
 
 template <typename T>
@@ -203,34 +223,39 @@ __device__ __forceinline__ uint32_t payload32_generic(const uint8_t *lds, const 
         if (k < K && pc >= 0) v = ld16<NT>(reinterpret_cast<const uint4 *>(a0 + (uint64_t)pc));
         return v;
     };
+    // edge handling (crc_gpu_mask.h) for the piece of step k < K
+    auto prep = [&](int64_t k, uint4 v) -> uint4 {
+        const int64_t pc = r0 + k * step + lane_off;
+        if (!mck_piece_clean(pc, hs, he, 4)) {
+            const int64_t lo = pc - hs;
+            v.x = mck_mask32(v.x, lo, ilen, init);
+            v.y = mck_mask32(v.y, lo + 4, ilen, init);
+            v.z = mck_mask32(v.z, lo + 8, ilen, init);
+            v.w = mck_mask32(v.w, lo + 12, ilen, init);
+        }
+        return v;
+    };
 
-    uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
     uint4 ring[kRing];
 #pragma unroll
     for (int u = 0; u < kRing; u++) ring[u] = fetch(u);
+    uint32_t x0 = 0, x1 = 0, x2 = 0, x3 = 0;
     for (int64_t k = 0; k < kmax; k += kRing) {
 #pragma unroll
         for (int u = 0; u < kRing; u++) {
-            uint4 v = ring[u];
-            const int64_t kk = k + u;
-            ring[u] = fetch(kk + kRing);
-            if (kk < K) {
-                const int64_t pc = r0 + kk * step + lane_off;
-                if (!mck_piece_clean(pc, hs, he, 4)) {
-                    const int64_t lo = pc - hs;
-                    v.x = mck_mask32(v.x, lo, ilen, init);
-                    v.y = mck_mask32(v.y, lo + 4, ilen, init);
-                    v.z = mck_mask32(v.z, lo + 8, ilen, init);
-                    v.w = mck_mask32(v.w, lo + 12, ilen, init);
-                }
-                s0 = f32(lds, s0 ^ v.x, lc0, lc1);
-                s1 = f32(lds, s1 ^ v.y, lc0, lc1);
-                s2 = f32(lds, s2 ^ v.z, lc0, lc1);
-                s3 = f32(lds, s3 ^ v.w, lc0, lc1);
+            const int64_t j = k + u;
+            const uint4 raw = ring[u];
+            ring[u] = fetch(j + kRing);
+            if (j < K) {
+                const uint4 w = prep(j, raw);
+                x0 = f32s(lds, x0 ^ w.x, lc0, lc1);
+                x1 = f32s(lds, x1 ^ w.y, lc0, lc1);
+                x2 = f32s(lds, x2 ^ w.z, lc0, lc1);
+                x3 = f32s(lds, x3 ^ w.w, lc0, lc1);
             }
         }
     }
-    uint32_t x = combine32<LOG2G>(lds, s0, s1, s2, s3, gl);
+    uint32_t x = combine32<LOG2G>(lds, x0, x1, x2, x3, gl);
     x = op32(lds, 2 + LOG2G + (uint32_t)(a1 - ea), x);
     if (len < 4) x ^= pk->zinit[len];
     return x;
@@ -309,30 +334,42 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_batch_kernel(BatchArgs a) {
 
 // ----------------------------------------------------------------- CRC-64 --
 
-// s' = Z^(16G)(x) from 16 nibble tables; table 2p+h at (2p+h)*4 KiB, entry v
-// at v*256 B, lane copy at (lane%32)*8 B.
-__device__ __forceinline__ uint64_t f64(const uint8_t *lds, uint64_t x, uint32_t lc) {
+__device__ __forceinline__ uint64_t xor3_64(uint64_t a, uint64_t b, uint64_t c) {
+    return (uint64_t)xor3((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32)) << 32 |
+           xor3((uint32_t)a, (uint32_t)b, (uint32_t)c);
+}
+
+// XOR of 16 table words and one more value: 8 bitop3 per 32-bit half.
+__device__ __forceinline__ uint64_t xor17(const uint64_t *r, uint64_t extra) {
+    const uint64_t a = xor3_64(r[0], r[1], r[2]), b = xor3_64(r[3], r[4], r[5]), c = xor3_64(r[6], r[7], r[8]);
+    const uint64_t d = xor3_64(r[9], r[10], r[11]), e = xor3_64(r[12], r[13], r[14]);
+    return xor3_64(xor3_64(r[15], extra, a), xor3_64(b, c, d), e);
+}
+
+// Z^(16G)(x) ^ next from 16 nibble tables (next = 0 in the step loop); table 2p+h at (2p+h)*4 KiB, entry
+// v at v*256 B, lane copy at (lane%32)*8 B.
+__device__ __forceinline__ uint64_t f64x(const uint8_t *lds, uint64_t x, uint64_t next, uint32_t lc) {
     const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
     const uint32_t n0 = xl & 0x0F0F0F0Fu, n1 = (xl >> 4) & 0x0F0F0F0Fu;
     const uint32_t n2 = xh & 0x0F0F0F0Fu, n3 = (xh >> 4) & 0x0F0F0F0Fu;
-    uint64_t r = 0;
+    uint64_t r[16];
 #pragma unroll
     for (int b = 0; b < 4; b++) {
         const uint32_t sel = 0x0C0C0400u | ((uint32_t)b << 8);
-        r ^= lds64(lds, __builtin_amdgcn_perm(n0, lc, sel) + (2 * b + 0) * 4096);
-        r ^= lds64(lds, __builtin_amdgcn_perm(n1, lc, sel) + (2 * b + 1) * 4096);
-        r ^= lds64(lds, __builtin_amdgcn_perm(n2, lc, sel) + (2 * (b + 4) + 0) * 4096);
-        r ^= lds64(lds, __builtin_amdgcn_perm(n3, lc, sel) + (2 * (b + 4) + 1) * 4096);
+        r[4 * b + 0] = lds64(lds, __builtin_amdgcn_perm(n0, lc, sel) + (2 * b + 0) * 4096);
+        r[4 * b + 1] = lds64(lds, __builtin_amdgcn_perm(n1, lc, sel) + (2 * b + 1) * 4096);
+        r[4 * b + 2] = lds64(lds, __builtin_amdgcn_perm(n2, lc, sel) + (2 * (b + 4) + 0) * 4096);
+        r[4 * b + 3] = lds64(lds, __builtin_amdgcn_perm(n3, lc, sel) + (2 * (b + 4) + 1) * 4096);
     }
-    return r;
+    return xor17(r, next);
 }
 
 __device__ __forceinline__ uint64_t op64(const uint8_t *lds, uint32_t o, uint64_t x) {
     const uint32_t base = kL64Main + o * 2048;
-    uint64_t r = 0;
+    uint64_t r[16];
 #pragma unroll
-    for (int h = 0; h < 16; h++) r ^= lds64(lds, base + h * 128 + (uint32_t)(((x >> (4 * h)) & 15u) << 3));
-    return r;
+    for (int h = 0; h < 16; h++) r[h] = lds64(lds, base + h * 128 + (uint32_t)(((x >> (4 * h)) & 15u) << 3));
+    return xor17(r, 0);
 }
 
 template <int LOG2G>
@@ -356,15 +393,18 @@ __device__ void fill_lds64(uint8_t *lds, const crc64_gpu_pack_t *pk) {
     for (uint32_t d = threadIdx.x; d < nops; d += kBlock) l[kL64Main / 8 + d] = ops[d];
 }
 
+__device__ __forceinline__ uint64_t lo64(uint4 v) { return (uint64_t)v.y << 32 | v.x; }
+__device__ __forceinline__ uint64_t hi64(uint4 v) { return (uint64_t)v.w << 32 | v.z; }
+
 template <int LOG2G, bool NT>
 __device__ __forceinline__ uint64_t payload64_aligned(const uint8_t *lds, const uint8_t *p, uint64_t K, uint32_t gl,
                                                       uint32_t lc, uint64_t init) {
     constexpr int G = 1 << LOG2G;
     const uint4 *src = reinterpret_cast<const uint4 *>(p) + gl;
-    uint64_t s0 = gl == 0 ? init : 0ull, s1 = 0;
     uint4 ring[kRing];
 #pragma unroll
     for (int u = 0; u < kRing; u++) ring[u] = (uint64_t)u < K ? ld16<NT>(src + (uint64_t)u * G) : make_uint4(0, 0, 0, 0);
+    uint64_t x0 = gl == 0 ? init : 0ull, x1 = 0;
     for (uint64_t k = 0; k < K; k += kRing) {
 #pragma unroll
         for (int u = 0; u < kRing; u++) {
@@ -372,12 +412,12 @@ __device__ __forceinline__ uint64_t payload64_aligned(const uint8_t *lds, const 
             const uint64_t kn = k + u + kRing;
             if (kn < K) ring[u] = ld16<NT>(src + kn * G);
             if (k + u < K) {
-                s0 = f64(lds, s0 ^ ((uint64_t)v.y << 32 | v.x), lc);
-                s1 = f64(lds, s1 ^ ((uint64_t)v.w << 32 | v.z), lc);
+                x0 = f64x(lds, x0 ^ lo64(v), 0, lc);
+                x1 = f64x(lds, x1 ^ hi64(v), 0, lc);
             }
         }
     }
-    return combine64<LOG2G>(lds, s0, s1, gl);
+    return combine64<LOG2G>(lds, x0, x1, gl);
 }
 
 template <int LOG2G, bool NT>
@@ -402,31 +442,37 @@ __device__ __forceinline__ uint64_t payload64_generic(const uint8_t *lds, const 
         if (k < K && pc >= 0) v = ld16<NT>(reinterpret_cast<const uint4 *>(a0 + (uint64_t)pc));
         return v;
     };
+    // edge handling (crc_gpu_mask.h) for the piece of step k < K
+    auto prep = [&](int64_t k, uint4 v, uint64_t *w0, uint64_t *w1) {
+        const int64_t pc = r0 + k * step + lane_off;
+        *w0 = lo64(v);
+        *w1 = hi64(v);
+        if (!mck_piece_clean(pc, hs, he, 8)) {
+            const int64_t lo = pc - hs;
+            *w0 = mck_mask64(*w0, lo, ilen, init);
+            *w1 = mck_mask64(*w1, lo + 8, ilen, init);
+        }
+    };
 
-    uint64_t s0 = 0, s1 = 0;
     uint4 ring[kRing];
 #pragma unroll
     for (int u = 0; u < kRing; u++) ring[u] = fetch(u);
+    uint64_t x0 = 0, x1 = 0;
     for (int64_t k = 0; k < kmax; k += kRing) {
 #pragma unroll
         for (int u = 0; u < kRing; u++) {
-            const uint4 v = ring[u];
-            const int64_t kk = k + u;
-            ring[u] = fetch(kk + kRing);
-            if (kk < K) {
-                const int64_t pc = r0 + kk * step + lane_off;
-                uint64_t w0 = (uint64_t)v.y << 32 | v.x, w1 = (uint64_t)v.w << 32 | v.z;
-                if (!mck_piece_clean(pc, hs, he, 8)) {
-                    const int64_t lo = pc - hs;
-                    w0 = mck_mask64(w0, lo, ilen, init);
-                    w1 = mck_mask64(w1, lo + 8, ilen, init);
-                }
-                s0 = f64(lds, s0 ^ w0, lc);
-                s1 = f64(lds, s1 ^ w1, lc);
+            const int64_t j = k + u;
+            const uint4 raw = ring[u];
+            ring[u] = fetch(j + kRing);
+            if (j < K) {
+                uint64_t w0, w1;
+                prep(j, raw, &w0, &w1);
+                x0 = f64x(lds, x0 ^ w0, 0, lc);
+                x1 = f64x(lds, x1 ^ w1, 0, lc);
             }
         }
     }
-    uint64_t x = combine64<LOG2G>(lds, s0, s1, gl);
+    uint64_t x = combine64<LOG2G>(lds, x0, x1, gl);
     x = op64(lds, 1 + LOG2G + (uint32_t)(a1 - ea), x);
     if (len < 8) x ^= pk->zinit[len];
     return x;
