@@ -23,6 +23,8 @@ SHAPES = {
     "metric": ("crc32c", 65536, 65536, 0x4D43310000000005),
     "c2": ("crc32c", 65536, 4096, 0x4D43310000000002),
     "c3": ("crc64", 8192, 1 << 20, 0x4D43310000000003),
+    "c4": ("crc32c", 262144, None, 0x4D43310000000004),   # offsets table, U[64 B, 64 KiB]
+    "c4_64": ("crc64", 262144, None, 0x4D43310000000004),
 }
 
 
@@ -64,9 +66,20 @@ def main():
     configs = args.config.split(",")
     for cfg in configs:
         method, count, length, seed = SHAPES[cfg]
-        data = torch.empty(count * length + 64, dtype=torch.uint8, device="cuda")
-        G.fill_splitmix(data, seed)
-        ref = G.checksum_fixed(method, data, length, count=count)
+        offs = None
+        if length is None:
+            from oracle import oracle as O
+            off_h = O.varlen_offsets(seed, count)
+            nbytes = int(off_h[-1])
+            data = torch.empty(nbytes + 64, dtype=torch.uint8, device="cuda")
+            offs = torch.from_numpy(off_h.astype(np.int64)).cuda()
+            G.fill_splitmix(data, seed)
+            ref = G.checksum_offsets(method, data, offs, offsets_host=off_h)
+        else:
+            nbytes = count * length
+            data = torch.empty(count * length + 64, dtype=torch.uint8, device="cuda")
+            G.fill_splitmix(data, seed)
+            ref = G.checksum_fixed(method, data, length, count=count)
         torch.cuda.synchronize()
         stream = torch.cuda.current_stream()
         h = stream.cuda_stream
@@ -82,8 +95,12 @@ def main():
                        for _ in range(args.iters)]
                 for a, b in evs:
                     a.record(stream)
-                    rc = L.mchecksum_gpu_checksum_fixed(method.encode(), data.data_ptr(), length, length, count,
-                                                        o.data_ptr(), h)
+                    if offs is None:
+                        rc = L.mchecksum_gpu_checksum_fixed(method.encode(), data.data_ptr(), length, length, count,
+                                                            o.data_ptr(), h)
+                    else:
+                        rc = L.mchecksum_gpu_checksum_offsets(method.encode(), data.data_ptr(), offs.data_ptr(),
+                                                              count, o.data_ptr(), h)
                     b.record(stream)
                     assert rc == 0
                 torch.cuda.synchronize()
@@ -93,7 +110,6 @@ def main():
                     times[n] += [a.elapsed_time(b) for a, b in evs]
         for n, o in zip(names, outs):
             assert torch.equal(o, ref), f"variant {n} differs from the default library"
-        nbytes = count * length
         res = {}
         for n in names:
             t = np.array(times[n])

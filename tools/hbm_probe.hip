@@ -1,36 +1,54 @@
-// hbm_probe.hip -- DIAGNOSTIC ONLY (not part of libmchecksum): the HBM read
-// ceiling for the CRC kernels' access pattern.  Same grid (one 1024-thread
-// workgroup per CU, a wave per 64 KiB payload, 16-B lanes, 4 loads in flight),
-// same load policy, but the "compute" is a single XOR per dword.
+// hbm_probe.hip -- DIAGNOSTIC ONLY (not part of libmchecksum): HBM read ceiling
+// for access patterns the batch kernels could use.  "compute" is one XOR per
+// dword.  mode 0 = the kernels' mapping (one 64 KiB payload per wave, 1 KiB
+// steps); mode 1 = linear sweep (all waves walk consecutive 1 KiB chunks).
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 
-template <bool NT>
-__global__ __launch_bounds__(1024, 1) void probe(const uint8_t *base, uint64_t len, uint64_t count, uint32_t *out) {
+template <bool NT, int MODE, int UNR>
+__global__ __launch_bounds__(1024) void probe(const uint8_t *base, uint64_t len, uint64_t count, uint32_t *out) {
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = blockIdx.x * 16 + (threadIdx.x >> 6);
-    const uint32_t nw = gridDim.x * 16;
+    const uint32_t wpb = blockDim.x >> 6;
+    const uint32_t wave = blockIdx.x * wpb + (threadIdx.x >> 6);
+    const uint32_t nw = gridDim.x * wpb;
     uint32_t acc = 0;
-    for (uint64_t p = wave; p < count; p += nw) {
-        const u32x4_t *src = reinterpret_cast<const u32x4_t *>(base + p * len) + lane;
-        const uint64_t K = len >> 10;
-#pragma unroll 4
-        for (uint64_t k = 0; k < K; k++) {
-            u32x4_t v = NT ? __builtin_nontemporal_load(src + k * 64) : src[k * 64];
+    if (MODE == 0) {
+        for (uint64_t p = wave; p < count; p += nw) {
+            const u32x4_t *src = reinterpret_cast<const u32x4_t *>(base + p * len) + lane;
+            const uint64_t K = len >> 10;
+#pragma unroll UNR
+            for (uint64_t k = 0; k < K; k++) {
+                u32x4_t v = NT ? __builtin_nontemporal_load(src + k * 64) : src[k * 64];
+                acc ^= v.x ^ v.y ^ v.z ^ v.w;
+            }
+        }
+    } else {
+        const uint64_t chunks = (len * count) >> 10;
+        const u32x4_t *src = reinterpret_cast<const u32x4_t *>(base) + lane;
+#pragma unroll UNR
+        for (uint64_t c = wave; c < chunks; c += nw) {
+            u32x4_t v = NT ? __builtin_nontemporal_load(src + c * 64) : src[c * 64];
             acc ^= v.x ^ v.y ^ v.z ^ v.w;
         }
     }
     if (acc == 0x12345678u) out[0] = acc;  // keep loads live
 }
 
-extern "C" int hbm_probe(const void *base, uint64_t len, uint64_t count, void *out, int nt, int blocks, void *stream) {
-    if (nt)
-        hipLaunchKernelGGL(probe<true>, dim3(blocks), dim3(1024), 0, (hipStream_t)stream, (const uint8_t *)base, len,
-                           count, (uint32_t *)out);
-    else
-        hipLaunchKernelGGL(probe<false>, dim3(blocks), dim3(1024), 0, (hipStream_t)stream, (const uint8_t *)base, len,
-                           count, (uint32_t *)out);
+typedef void (*pk)(const uint8_t *, uint64_t, uint64_t, uint32_t *);
+template <int MODE, int UNR>
+static pk pick(int nt) { return nt ? probe<true, MODE, UNR> : probe<false, MODE, UNR>; }
+
+extern "C" int hbm_probe2(const void *base, uint64_t len, uint64_t count, void *out, int nt, int mode, int unr,
+                          int blocks, int threads, void *stream) {
+    pk k;
+    if (mode == 0) k = unr == 8 ? pick<0, 8>(nt) : pick<0, 4>(nt);
+    else k = unr == 8 ? pick<1, 8>(nt) : pick<1, 4>(nt);
+    hipLaunchKernelGGL(k, dim3(blocks), dim3(threads), 0, (hipStream_t)stream, (const uint8_t *)base, len, count,
+                       (uint32_t *)out);
     return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+extern "C" int hbm_probe(const void *base, uint64_t len, uint64_t count, void *out, int nt, int blocks, void *stream) {
+    return hbm_probe2(base, len, count, out, nt, 0, 4, blocks, 1024, stream);
 }
