@@ -59,6 +59,30 @@ constexpr uint32_t kL32Bytes = kL32Main + CRC32_NOPS_MAX * 512;
 // CRC-64 LDS map: [0,64K) main nibble tables x32 copies; then op nibble tables.
 constexpr uint32_t kL64Main = 65536;
 constexpr uint32_t kL64Bytes = kL64Main + CRC64_NOPS_MAX * 2048;
+// CRC-64 over large aligned payloads is latency-bound at one workgroup per CU
+// (SQ_WAIT_INST_ANY 40% of wave time).  Its "split" launch shape keeps only the
+// 64 KiB main tables in LDS and reads the combine operators (touched once per
+// payload) from global memory, so two workgroups of MCK_BLOCK64 threads fit a
+// CU.  Variable-length batches keep the operators in LDS (many combines).
+#ifndef MCK_CRC64_SPLIT
+#define MCK_CRC64_SPLIT 1
+#endif
+#ifndef MCK_BLOCK64
+#define MCK_BLOCK64 1024
+#endif
+
+template <int W, int MODE>
+struct Shape {
+    static constexpr bool ops_global = W == 64 && MODE == 0 && MCK_CRC64_SPLIT;  // 0 = kFixedAligned
+    static constexpr int block = ops_global ? MCK_BLOCK64 : kBlock;
+    static constexpr int blocks_per_cu = ops_global ? 2 : 1;
+    static constexpr uint32_t lds64_bytes = ops_global ? kL64Main : kL64Bytes;
+};
+// single-argument aliases (a comma inside __launch_bounds__ splits the macro)
+template <int MODE>
+constexpr int kBlk64 = Shape<64, MODE>::block;
+template <int MODE>
+constexpr int kWpe64 = Shape<64, MODE>::blocks_per_cu * Shape<64, MODE>::block / 256;
 
 enum Mode : int { kFixedAligned = 0, kFixedGeneric = 1, kOffsets = 2 };
 
@@ -364,41 +388,52 @@ __device__ __forceinline__ uint64_t f64x(const uint8_t *lds, uint64_t x, uint64_
     return xor17(r, next);
 }
 
-__device__ __forceinline__ uint64_t op64(const uint8_t *lds, uint32_t o, uint64_t x) {
-    const uint32_t base = kL64Main + o * 2048;
+template <bool OG>
+__device__ __forceinline__ uint64_t op64(const uint8_t *lds, const crc64_gpu_pack_t *pk, uint32_t o, uint64_t x) {
     uint64_t r[16];
+    if constexpr (OG) {
+        const uint64_t *t = &pk->ops[o][0][0];
 #pragma unroll
-    for (int h = 0; h < 16; h++) r[h] = lds64(lds, base + h * 128 + (uint32_t)(((x >> (4 * h)) & 15u) << 3));
+        for (int h = 0; h < 16; h++) r[h] = t[h * 16 + ((x >> (4 * h)) & 15u)];
+    } else {
+        const uint32_t base = kL64Main + o * 2048;
+#pragma unroll
+        for (int h = 0; h < 16; h++) r[h] = lds64(lds, base + h * 128 + (uint32_t)(((x >> (4 * h)) & 15u) << 3));
+    }
     return xor17(r, 0);
 }
 
-template <int LOG2G>
-__device__ __forceinline__ uint64_t combine64(const uint8_t *lds, uint64_t s0, uint64_t s1, uint32_t gl) {
-    uint64_t x = s0 ^ op64(lds, 0, s1);
+template <int LOG2G, bool OG>
+__device__ __forceinline__ uint64_t combine64(const uint8_t *lds, const crc64_gpu_pack_t *pk, uint64_t s0, uint64_t s1,
+                                              uint32_t gl) {
+    uint64_t x = s0 ^ op64<OG>(lds, pk, 0, s1);
 #pragma unroll
     for (int k = 0; k < LOG2G; k++) {
         const uint64_t other = __shfl_xor(x, 1 << k, 64);
         const bool bit = (gl >> k) & 1u;
         const uint64_t lo = bit ? other : x, hi = bit ? x : other;
-        x = lo ^ op64(lds, 1 + k, hi);
+        x = lo ^ op64<OG>(lds, pk, 1 + k, hi);
     }
     return x;
 }
 
+template <int BLOCK, bool OG>
 __device__ void fill_lds64(uint8_t *lds, const crc64_gpu_pack_t *pk) {
     uint64_t *l = reinterpret_cast<uint64_t *>(lds);
-    for (uint32_t d = threadIdx.x; d < 8192u; d += kBlock) l[d] = pk->main[d >> 9][(d >> 5) & 15u];
-    const uint64_t *ops = &pk->ops[0][0][0];
-    const uint32_t nops = pk->nops * 256u;
-    for (uint32_t d = threadIdx.x; d < nops; d += kBlock) l[kL64Main / 8 + d] = ops[d];
+    for (uint32_t d = threadIdx.x; d < 8192u; d += BLOCK) l[d] = pk->main[d >> 9][(d >> 5) & 15u];
+    if constexpr (!OG) {
+        const uint64_t *ops = &pk->ops[0][0][0];
+        const uint32_t nops = pk->nops * 256u;
+        for (uint32_t d = threadIdx.x; d < nops; d += BLOCK) l[kL64Main / 8 + d] = ops[d];
+    }
 }
 
 __device__ __forceinline__ uint64_t lo64(uint4 v) { return (uint64_t)v.y << 32 | v.x; }
 __device__ __forceinline__ uint64_t hi64(uint4 v) { return (uint64_t)v.w << 32 | v.z; }
 
-template <int LOG2G, bool NT>
-__device__ __forceinline__ uint64_t payload64_aligned(const uint8_t *lds, const uint8_t *p, uint64_t K, uint32_t gl,
-                                                      uint32_t lc, uint64_t init) {
+template <int LOG2G, bool NT, bool OG>
+__device__ __forceinline__ uint64_t payload64_aligned(const uint8_t *lds, const crc64_gpu_pack_t *pk, const uint8_t *p,
+                                                      uint64_t K, uint32_t gl, uint32_t lc, uint64_t init) {
     constexpr int G = 1 << LOG2G;
     const uint4 *src = reinterpret_cast<const uint4 *>(p) + gl;
     uint4 ring[kRing];
@@ -417,7 +452,7 @@ __device__ __forceinline__ uint64_t payload64_aligned(const uint8_t *lds, const 
             }
         }
     }
-    return combine64<LOG2G>(lds, x0, x1, gl);
+    return combine64<LOG2G, OG>(lds, pk, x0, x1, gl);
 }
 
 template <int LOG2G, bool NT>
@@ -472,17 +507,19 @@ __device__ __forceinline__ uint64_t payload64_generic(const uint8_t *lds, const 
             }
         }
     }
-    uint64_t x = combine64<LOG2G>(lds, x0, x1, gl);
-    x = op64(lds, 1 + LOG2G + (uint32_t)(a1 - ea), x);
+    uint64_t x = combine64<LOG2G, false>(lds, pk, x0, x1, gl);
+    x = op64<false>(lds, pk, 1 + LOG2G + (uint32_t)(a1 - ea), x);
     if (len < 8) x ^= pk->zinit[len];
     return x;
 }
 
 template <int LOG2G, int MODE, bool VERIFY, bool NT>
-__global__ __launch_bounds__(kBlock, 1) void crc64_batch_kernel(BatchArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kL64Bytes];
+__global__ __launch_bounds__(kBlk64<MODE>, kWpe64<MODE>) void crc64_batch_kernel(BatchArgs a) {
+    using S = Shape<64, MODE>;
+    constexpr int kWPB = S::block / 64;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[S::lds64_bytes];
     const crc64_gpu_pack_t *pk = reinterpret_cast<const crc64_gpu_pack_t *>(a.pack);
-    fill_lds64(lds, pk);
+    fill_lds64<S::block, S::ops_global>(lds, pk);
     __syncthreads();
 
     constexpr int PPW = 64 >> LOG2G;
@@ -490,8 +527,8 @@ __global__ __launch_bounds__(kBlock, 1) void crc64_batch_kernel(BatchArgs a) {
     const uint32_t gl = lane & ((1u << LOG2G) - 1u), grp = lane >> LOG2G;
     const uint32_t lc = (lane & 31u) << 3;
     const uint64_t xorout = pk->xorout;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
-    const uint32_t nw = gridDim.x * kWavesPerBlock;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWPB + (threadIdx.x >> 6));
+    const uint32_t nw = gridDim.x * kWPB;
 
     if (MODE == kOffsets) {
         uint64_t first, last;
@@ -509,7 +546,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc64_batch_kernel(BatchArgs a) {
         const uint64_t pc = act ? p : a.count - 1;
         uint64_t x;
         if (MODE == kFixedAligned)
-            x = payload64_aligned<LOG2G, NT>(lds, a.base + pc * a.stride, a.len >> (4 + LOG2G), gl, lc, pk->init);
+            x = payload64_aligned<LOG2G, NT, S::ops_global>(lds, pk, a.base + pc * a.stride, a.len >> (4 + LOG2G), gl, lc, pk->init);
         else
             x = payload64_generic<LOG2G, NT>(lds, pk, a.base + pc * a.stride, a.len, gl, lc);
         if (act && gl == 0) emit<uint64_t, VERIFY>(a, p, x ^ xorout);
@@ -624,20 +661,26 @@ int choose_log2g(size_t len) {
 
 typedef void (*kern_t)(BatchArgs);
 
+struct KLaunch {
+    kern_t k;
+    int block, blocks_per_cu;
+};
+
 template <int W, int LOG2G, int MODE, bool VERIFY, bool NT = false>
-kern_t kernel_ptr() {
-    if constexpr (W == 32) return crc32c_batch_kernel<LOG2G, MODE, VERIFY, NT>;
-    else return crc64_batch_kernel<LOG2G, MODE, VERIFY, NT>;
+KLaunch kernel_ptr() {
+    using S = Shape<W, MODE>;
+    if constexpr (W == 32) return {crc32c_batch_kernel<LOG2G, MODE, VERIFY, NT>, S::block, S::blocks_per_cu};
+    else return {crc64_batch_kernel<LOG2G, MODE, VERIFY, NT>, S::block, S::blocks_per_cu};
 }
 
 template <int W, int LOG2G>
-kern_t pick_fixed_lg(bool aligned, bool nt) {
+KLaunch pick_fixed_lg(bool aligned, bool nt) {
     if (!aligned) return kernel_ptr<W, LOG2G, kFixedGeneric, false>();
     return nt ? kernel_ptr<W, LOG2G, kFixedAligned, false, true>() : kernel_ptr<W, LOG2G, kFixedAligned, false>();
 }
 
 template <int W>
-kern_t pick_fixed(int log2g, bool aligned, bool nt) {
+KLaunch pick_fixed(int log2g, bool aligned, bool nt) {
     switch (log2g) {
         case 0: return pick_fixed_lg<W, 0>(aligned, nt);
         case 1: return pick_fixed_lg<W, 1>(aligned, nt);
@@ -657,16 +700,17 @@ bool use_nt(uint64_t batch_bytes) {
     return batch_bytes >= (512ull << 20);
 }
 
-int launch(kern_t k, const BatchArgs &a, unsigned blocks, void *stream) {
-    hipLaunchKernelGGL(k, dim3(blocks), dim3(kBlock), 0, (hipStream_t)stream, a);
+int launch(const KLaunch &kl, const BatchArgs &a, unsigned blocks, void *stream) {
+    hipLaunchKernelGGL(kl.k, dim3(blocks), dim3(kl.block), 0, (hipStream_t)stream, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_err(e, "kernel launch");
     return MCHECKSUM_GPU_OK;
 }
 
-unsigned grid_for(const DevCtx *c, uint64_t waves_needed) {
-    uint64_t blocks = (waves_needed + kWavesPerBlock - 1) / kWavesPerBlock;
-    if (blocks > (uint64_t)c->cus) blocks = (uint64_t)c->cus;
+unsigned grid_for(const DevCtx *c, uint64_t waves_needed, const KLaunch &kl) {
+    const uint64_t wpb = (uint64_t)kl.block / 64;
+    uint64_t blocks = (waves_needed + wpb - 1) / wpb;
+    if (blocks > (uint64_t)c->cus * kl.blocks_per_cu) blocks = (uint64_t)c->cus * kl.blocks_per_cu;
     return blocks ? (unsigned)blocks : 1u;
 }
 
@@ -700,7 +744,7 @@ int do_offsets(const char *method, const void *base, const uint64_t *offsets, si
     a.status = status;
     a.mismatches = mism;
     a.pack = pack;
-    kern_t k;
+    KLaunch k;
     // The offsets table stays on the device, so size the batch by its count:
     // 8192+ payloads of the C4 mix are ~270 MB and up.
     const bool nt = use_nt(count >= 8192 ? (1ull << 40) : 0);
@@ -710,7 +754,7 @@ int do_offsets(const char *method, const void *base, const uint64_t *offsets, si
     else
         k = verify ? (nt ? kernel_ptr<64, 6, kOffsets, true, true>() : kernel_ptr<64, 6, kOffsets, true>())
                    : (nt ? kernel_ptr<64, 6, kOffsets, false, true>() : kernel_ptr<64, 6, kOffsets, false>());
-    return launch(k, a, grid_for(c, count), stream);
+    return launch(k, a, grid_for(c, count, k), stream);
 }
 
 }  // namespace
@@ -767,9 +811,9 @@ int mchecksum_gpu_checksum_fixed(const char *hash_method, const void *dev_base, 
     a.out = dev_out;
     a.pack = pack;
     const bool nt = use_nt((uint64_t)len * count);
-    kern_t k = width == 32 ? pick_fixed<32>(lg, aligned, nt) : pick_fixed<64>(lg, aligned, nt);
+    const KLaunch k = width == 32 ? pick_fixed<32>(lg, aligned, nt) : pick_fixed<64>(lg, aligned, nt);
     const uint64_t ppw = 64u >> lg;
-    return launch(k, a, grid_for(c, (count + ppw - 1) / ppw), stream);
+    return launch(k, a, grid_for(c, (count + ppw - 1) / ppw, k), stream);
 }
 
 int mchecksum_gpu_checksum_offsets(const char *hash_method, const void *dev_base, const uint64_t *dev_offsets,

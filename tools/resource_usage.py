@@ -3,7 +3,7 @@ import re, subprocess, sys
 path = sys.argv[1] if len(sys.argv) > 1 else "build/resource_usage.txt"
 rows, cur = [], None
 for line in open(path):
-    m = re.search(r"remark: \S+:\d+:\d+: (.*?) \[-Rpass", line)
+    m = re.search(r"(?:remark: )?\S+:\d+:\d+: (?:remark: )?(.*?) \[-Rpass", line)
     if not m:
         continue
     txt = m.group(1).strip()
