@@ -61,7 +61,7 @@ clean:
 
 # A/B variants of the batch kernels (tools/ab_variants.py).  Each is a full
 # libmchecksum built with different tuning macros.
-VARIANTS := base:-DMCK_RING=4 nosplit:-DMCK_CRC64_SPLIT=0 split1024:-DMCK_BLOCK64=1024 split512:-DMCK_BLOCK64=512
+VARIANTS := base:-DMCK_RING=4 ring6:-DMCK_RING=6 ring8:-DMCK_RING=8
 variants: $(COBJS) | $(BUILD)
 	mkdir -p $(BUILD)/variants
 	@for v in $(VARIANTS); do n=$${v%%:*}; f=$$(echo $${v#*:} | tr , " "); \
