@@ -79,6 +79,23 @@ mchecksum_gpu_verify_offsets(const char *hash_method, const void *dev_base,
     const uint64_t *dev_offsets, size_t count, const void *dev_expected,
     uint8_t *dev_status, uint32_t *dev_mismatches, void *stream);
 
+/* Batched verify of received RPC messages in place.
+ * Message i = dev_buf[dev_msg_offsets[i], dev_msg_offsets[i+1]) as it sits in
+ * an NA multi-recv buffer (src/mercury_core.c:2092-2132, 4667-4714): headers,
+ * then the serialized payload from payload_offset on.  The expected CRC is
+ * the network-order u32 at hash_offset -- in Mercury the HG header's payload
+ * hash (src/mercury_header.c:111-112) right after the 16-byte core header, so
+ * hash_offset = 16 and payload_offset = 20 for HG_INPUT without user offset.
+ * dev_status[i] = 1 when the payload CRC differs (what hg_get_struct reports
+ * as HG_CHECKSUM_ERROR, src/mercury.c:565-573) or the message is shorter than
+ * payload_offset; *dev_mismatches is incremented per failure.  crc32c only
+ * (the header slot is 32 bits). */
+MCHECKSUM_PUBLIC int
+mchecksum_gpu_verify_messages(const char *hash_method, const void *dev_buf,
+    const uint64_t *dev_msg_offsets, size_t count, size_t payload_offset,
+    size_t hash_offset, uint8_t *dev_status, uint32_t *dev_mismatches,
+    void *stream);
+
 /* Lanes cooperating on one payload that checksum_fixed would choose for
  * this length (1..64), for reporting; -1 on error. */
 MCHECKSUM_PUBLIC int

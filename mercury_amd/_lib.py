@@ -20,7 +20,7 @@ BENCH_LIB_PATH = os.path.join(LIB_DIR, "libmchecksum_bench.so")
 STREAMING_SYMBOLS = ("mchecksum_init", "mchecksum_destroy", "mchecksum_reset", "mchecksum_get_size",
                      "mchecksum_get", "mchecksum_update")
 GPU_SYMBOLS = ("mchecksum_gpu_available", "mchecksum_gpu_prepare", "mchecksum_gpu_checksum_fixed",
-               "mchecksum_gpu_checksum_offsets", "mchecksum_gpu_verify_offsets",
+               "mchecksum_gpu_checksum_offsets", "mchecksum_gpu_verify_offsets", "mchecksum_gpu_verify_messages",
                "mchecksum_gpu_lanes_per_payload", "mchecksum_gpu_last_error")
 
 _lib = None
@@ -60,6 +60,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     L.mchecksum_gpu_verify_offsets.argtypes = [c_char_p, c_void_p, c_void_p, c_size_t, c_void_p, c_void_p,
                                                c_void_p, c_void_p]
     L.mchecksum_gpu_verify_offsets.restype = c_int
+    L.mchecksum_gpu_verify_messages.argtypes = [c_char_p, c_void_p, c_void_p, c_size_t, c_size_t, c_size_t, c_void_p,
+                                                c_void_p, c_void_p]
+    L.mchecksum_gpu_verify_messages.restype = c_int
     L.mchecksum_gpu_lanes_per_payload.argtypes = [c_char_p, c_size_t]
     L.mchecksum_gpu_lanes_per_payload.restype = c_int
     L.mchecksum_gpu_last_error.argtypes = []

@@ -101,7 +101,16 @@ struct BatchArgs {
     uint8_t *status;
     uint32_t *mismatches;
     const void *pack;
+    // message mode (verify_messages): payload i = [offsets[i] + pay_off,
+    // offsets[i+1]), expected CRC = big-endian u32 at offsets[i] + hash_off
+    uint32_t msg, pay_off, hash_off;
 };
+
+// Network-order u32 at an arbitrary byte address (the HG header's payload
+// hash, src/mercury_header.c:111-112 writes it with htonl).
+__device__ __forceinline__ uint32_t load_be32(const uint8_t *q) {
+    return (uint32_t)q[0] << 24 | (uint32_t)q[1] << 16 | (uint32_t)q[2] << 8 | (uint32_t)q[3];
+}
 
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 
@@ -403,11 +412,22 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_batch_kernel(BatchArgs a) {
         uint64_t first, last;
         wave_range(a.offsets, a.count, wave, nw, &first, &last);
         for (uint64_t p = first; p < last; p++) {
-            const uint64_t o = a.offsets[p];
-            const uint64_t n = a.offsets[p + 1] - o;
+            const uint64_t m0 = a.offsets[p], m1 = a.offsets[p + 1];
+            // message mode: a message shorter than its headers fails verification
+            const bool short_msg = a.msg && m1 - m0 < a.pay_off;
+            const uint64_t o = a.msg ? (short_msg ? m1 : m0 + a.pay_off) : m0;
+            const uint64_t n = m1 - o;
             const uint32_t x = n < (1ull << 31) ? payload32_g64<NT>(lds, pk, a.base + o, n, gl, lc0, lc1)
                                                 : payload32_generic<LOG2G, NT>(lds, pk, a.base + o, n, gl, lc0, lc1);
-            if (gl == 0) emit<uint32_t, VERIFY>(a, p, x ^ xorout);
+            if (gl == 0) {
+                if (VERIFY && a.msg) {
+                    const bool bad = short_msg || load_be32(a.base + m0 + a.hash_off) != (x ^ xorout);
+                    if (a.status) a.status[p] = bad ? 1 : 0;
+                    if (bad && a.mismatches) atomicAdd(a.mismatches, 1u);
+                } else {
+                    emit<uint32_t, VERIFY>(a, p, x ^ xorout);
+                }
+            }
         }
         return;
     }
@@ -848,9 +868,12 @@ int prologue(const char *method, int log2g, int *width, DevCtx **c, const void *
 }
 
 int do_offsets(const char *method, const void *base, const uint64_t *offsets, size_t count, void *out,
-               const void *expected, uint8_t *status, uint32_t *mism, void *stream, bool verify) {
-    if ((!base && count) || !offsets || (!verify && !out && count) || (verify && !expected))
+               const void *expected, uint8_t *status, uint32_t *mism, void *stream, bool verify,
+               bool msg = false, size_t pay_off = 0, size_t hash_off = 0) {
+    if ((!base && count) || !offsets || (!verify && !out && count) || (verify && !msg && !expected))
         return set_err(MCHECKSUM_GPU_EINVAL, "NULL pointer argument%s%d");
+    if (msg && (hash_off + 4 > pay_off || pay_off > (1u << 30)))
+        return set_err(MCHECKSUM_GPU_EINVAL, "hash_offset + 4 must not exceed payload_offset%s%d");
     if (!mchecksum_gpu_available()) return set_err(MCHECKSUM_GPU_ENODEV, "no HIP device%s%d");
     int width = 0;
     DevCtx *c = nullptr;
@@ -867,6 +890,11 @@ int do_offsets(const char *method, const void *base, const uint64_t *offsets, si
     a.status = status;
     a.mismatches = mism;
     a.pack = pack;
+    a.msg = msg ? 1u : 0u;
+    a.pay_off = (uint32_t)pay_off;
+    a.hash_off = (uint32_t)hash_off;
+    if (msg && width != 32)
+        return set_err(MCHECKSUM_GPU_EMETHOD, "message verify carries a 32-bit header hash: crc32c only%s%d");
     KLaunch k;
     // The offsets table stays on the device, so size the batch by its count:
     // 8192+ payloads of the C4 mix are ~270 MB and up.
@@ -949,6 +977,13 @@ int mchecksum_gpu_verify_offsets(const char *hash_method, const void *dev_base, 
                                  uint32_t *dev_mismatches, void *stream) {
     return do_offsets(hash_method, dev_base, dev_offsets, count, nullptr, dev_expected, dev_status,
                       dev_mismatches, stream, true);
+}
+
+int mchecksum_gpu_verify_messages(const char *hash_method, const void *dev_buf, const uint64_t *dev_msg_offsets,
+                                  size_t count, size_t payload_offset, size_t hash_offset, uint8_t *dev_status,
+                                  uint32_t *dev_mismatches, void *stream) {
+    return do_offsets(hash_method, dev_buf, dev_msg_offsets, count, nullptr, nullptr, dev_status, dev_mismatches,
+                      stream, true, true, payload_offset, hash_offset);
 }
 
 const char *mchecksum_gpu_last_error(void) { return t_err; }

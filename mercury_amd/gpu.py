@@ -140,6 +140,24 @@ def verify_offsets(method: str, data: torch.Tensor, offsets: torch.Tensor, expec
     return status, mism
 
 
+def verify_messages(data: torch.Tensor, msg_offsets: torch.Tensor, payload_offset: int = 20, hash_offset: int = 16,
+                    method: str = "crc32c", stream=None, offsets_host=None):
+    """Verify received RPC messages in place: payload after payload_offset,
+    expected CRC = network-order u32 at hash_offset (Mercury: 16 B core header,
+    4 B HG header).  Returns (status uint8 per message: 1 = fails, count)."""
+    _check_device_u8(data, "data")
+    _check_offsets(data, msg_offsets, offsets_host)
+    count = msg_offsets.numel() - 1
+    status = torch.empty(max(count, 0), dtype=torch.uint8, device=data.device)
+    mism = torch.zeros(1, dtype=torch.int32, device=data.device)
+    rc = _lib().mchecksum_gpu_verify_messages(method.encode(), data.data_ptr(), msg_offsets.data_ptr(), count,
+                                              payload_offset, hash_offset, status.data_ptr(), mism.data_ptr(),
+                                              _stream_handle(stream))
+    if rc != 0:
+        _err(rc, "mchecksum_gpu_verify_messages")
+    return status, mism
+
+
 def fill_splitmix(t: torch.Tensor, seed: int, first_word: int = 0, stream=None) -> torch.Tensor:
     """Fill a device tensor with the synthetic payload bytes of SURVEY.md 8(d)."""
     _check_device_u8(t, "tensor")
