@@ -23,7 +23,7 @@ METHODS = ["crc32c", "crc64"]
 def _dev_bytes(torch, host: np.ndarray, pad: int = 64):
     t = torch.zeros(host.size + pad, dtype=torch.uint8, device="cuda")
     if host.size:
-        t[:host.size].copy_(torch.from_numpy(host))
+        t[:host.size].copy_(torch.from_numpy(np.array(host, dtype=np.uint8)))
     return t
 
 
