@@ -18,7 +18,7 @@ BENCHLIB  := $(LIBDIR)/libmchecksum_bench.so
 COBJS     := $(BUILD)/mchecksum_cpu.o $(BUILD)/mchecksum_models.o $(BUILD)/crc_tables.o
 GOBJS     := $(BUILD)/mchecksum_gpu.o
 
-all: $(LIB) $(BENCHLIB) oracle
+all: $(LIB) $(BENCHLIB) oracle $(BUILD)/c1_bench
 
 $(BUILD) $(LIBDIR):
 	mkdir -p $@
@@ -41,6 +41,9 @@ $(BENCHLIB): $(BUILD)/bench_datagen.o | $(LIBDIR)
 
 oracle:
 	$(MAKE) -C oracle
+
+$(BUILD)/c1_bench: tools/c1_bench.c include/mchecksum.h $(LIB) | $(BUILD)
+	$(CC) -O2 -std=c11 -Wall -Iinclude $< -o $@ -L$(LIBDIR) -lmchecksum -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)'
 
 # CPU-only artefacts (no hipcc needed): streaming API for host tests.
 cpu: $(LIBDIR)/libmchecksum_cpu.so

@@ -36,6 +36,8 @@ CONFIGS = {
     "c2": ("crc32c", 65536, 4096, 0x4D43310000000002, "fixed"),
     "c3": ("crc64", 8192, 1 << 20, 0x4D43310000000003, "fixed"),
     "c4": ("crc32c", 262144, None, 0x4D43310000000004, "offsets"),
+    # BASELINE configs[0]: host CPU, through the drop-in streaming API
+    "c1": ("crc32c", 1024, 4096, 0x4D43310000000001, "cpu"),
 }
 
 
@@ -55,6 +57,8 @@ def parse():
 
 def main():
     args = parse()
+    if CONFIGS[args.config][4] == "cpu":
+        return bench_c1(args)
     import torch
     import torch.distributed as dist
 
@@ -198,6 +202,49 @@ def main():
         dist.barrier()
         dist.destroy_process_group()
     return result
+
+
+def bench_c1(args):
+    """C1 (BASELINE configs[0]): CRC-32C of 1024 x 4 KiB host buffers through
+    libmchecksum's streaming API as Mercury's proc layer drives it
+    (tools/c1_bench.c, C, one thread).  No GPU.  The reference's own mchecksum
+    is absent, so the baseline beside it is the oracle's SSE4.2 path."""
+    import struct
+    import subprocess
+    from oracle import oracle as O
+    method, count, length, seed, _ = CONFIGS["c1"]
+    exe = os.path.join(ROOT, "build", "c1_bench")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-s", "-C", ROOT, "build/c1_bench"], check=True)
+    host = O.splitmix_bytes(count * length, seed)
+    steps = max(args.steps, 200)
+    r = subprocess.run([exe, str(count), str(length), str(steps), str(args.warmup)], input=host.tobytes(),
+                       capture_output=True, check=True)
+    el, first, xsum = r.stdout.decode().split()
+    el = float(el)
+    want = [O.crc(method, struct.pack("<I", length) + host[i * length:(i + 1) * length].tobytes())
+            for i in range(count)]
+    wx = 0
+    for w in want:
+        wx ^= w
+    ok = int(first) == want[0] and int(xsum) == wx
+    ref_t0 = time.perf_counter()
+    for _ in range(steps):
+        O.batch_fixed(method, host, length, length, count, variant="sse42", nthreads=1)
+    ref_el = time.perf_counter() - ref_t0
+    res = {"metric": "GiB/s checksummed on the host CPU through the mchecksum API, c1",
+           "value": round(count * (length + 4) * steps / el / 2**30, 3), "unit": "GiB/s", "n_gpus": 0,
+           "steps": steps, "warmup": args.warmup, "ms_per_step": round(el / steps * 1e3, 4),
+           "higher_is_better": True, "scaling": "none", "vs_baseline": None, "dtype": "u8",
+           "data": "synthetic (splitmix64 bytes)",
+           "config": {"workload": "crc32c, 1024 x (4 B length field + 4 KiB raw bytes) via reset/update/update/get",
+                      "threads": 1, "driver": "tools/c1_bench.c"},
+           "parity": "bit-exact (all 1024 payloads: first + xor-sum vs oracle)" if ok else "MISMATCH",
+           "cpu_baseline": {"value": round(count * length * steps / ref_el / 2**30, 3), "unit": "GiB/s",
+                            "cores": 1, "kind": "port", "variant": "x86 SSE4.2 crc32 instruction (oracle)",
+                            "sample": f"{steps} passes over the same 1024 x 4 KiB buffers"}}
+    print(json.dumps(res), flush=True)
+    return res
 
 
 def cpu_baseline(method, seed, length, budget_s):
