@@ -50,7 +50,6 @@ namespace {
 #define MCK_BITOP3 1
 #endif
 constexpr int kBlock = MCK_BLOCK;  // 1024 = 16 waves: 4 per SIMD
-constexpr int kWavesPerBlock = kBlock / 64;
 constexpr int kRing = MCK_RING;  // dwordx4 pieces in flight per lane
 // Offsets batches (one payload per wave, ~32 KiB average) want a deeper ring:
 // 8 measured +4% over 4 on C4, while 8 costs 1-5% on the aligned batches.
@@ -62,6 +61,20 @@ constexpr int kRingOff = MCK_RING_OFFSETS;
 // CRC-32C LDS map: [0,128K) main byte tables x32 copies; then op nibble tables.
 constexpr uint32_t kL32Main = 131072;
 constexpr uint32_t kL32Bytes = kL32Main + CRC32_NOPS_MAX * 512;
+// Light layout for small batches: the 4 byte tables unreplicated (4 KiB, so
+// the per-workgroup LDS fill is 16 KiB instead of 140 KiB) and 256-thread
+// workgroups spread over every CU; lookups may bank-conflict, which a small
+// batch never notices.
+constexpr uint32_t kL32LightMain = 4096;
+constexpr uint32_t kL32LightBytes = kL32LightMain + CRC32_NOPS_MAX * 512;
+constexpr int kLightBlock = 256;
+
+// CRC-32C table access policy: Tab32<false> = 32x-replicated conflict-free
+// layout (throughput), Tab32<true> = light layout (latency of small batches).
+template <bool LIGHT>
+struct Tab32 {
+    const uint8_t *lds;
+};
 // CRC-64 LDS map: [0,64K) main nibble tables x32 copies; then op nibble tables.
 constexpr uint32_t kL64Main = 65536;
 constexpr uint32_t kL64Bytes = kL64Main + CRC64_NOPS_MAX * 2048;
@@ -77,11 +90,11 @@ constexpr uint32_t kL64Bytes = kL64Main + CRC64_NOPS_MAX * 2048;
 #define MCK_BLOCK64 1024
 #endif
 
-template <int W, int MODE>
+template <int W, int MODE, bool LIGHT = false>
 struct Shape {
     static constexpr bool ops_global = W == 64 && MODE == 0 && MCK_CRC64_SPLIT;  // 0 = kFixedAligned
-    static constexpr int block = ops_global ? MCK_BLOCK64 : kBlock;
-    static constexpr int blocks_per_cu = ops_global ? 2 : 1;
+    static constexpr int block = LIGHT ? kLightBlock : ops_global ? MCK_BLOCK64 : kBlock;
+    static constexpr int blocks_per_cu = LIGHT ? 8 : ops_global ? 2 : 1;
     static constexpr uint32_t lds64_bytes = ops_global ? kL64Main : kL64Bytes;
 };
 // single-argument aliases (a comma inside __launch_bounds__ splits the macro)
@@ -154,24 +167,30 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 // a sub-stream costs 4 v_perm + 2 v_bitop3 (+1 XOR with the data word) per
 // 4 bytes.  (Folding the next word into this XOR tree instead -- a look-ahead
 // pipeline -- measured 7% slower on the headline batch, profiles/r01/ab3.log.)
-__device__ __forceinline__ uint32_t f32s(const uint8_t *lds, uint32_t x, uint32_t lc0, uint32_t lc1) {
+__device__ __forceinline__ uint32_t f32s(Tab32<false> t, uint32_t x, uint32_t lc0, uint32_t lc1) {
     const uint32_t a0 = __builtin_amdgcn_perm(x, lc0, 0x0C020400u);
     const uint32_t a1 = __builtin_amdgcn_perm(x, lc0, 0x0C020500u);
     const uint32_t a2 = __builtin_amdgcn_perm(x, lc1, 0x0C020600u);
     const uint32_t a3 = __builtin_amdgcn_perm(x, lc1, 0x0C020700u);
-    return xor3(lds32(lds, a0), lds32(lds, a1 + 128), lds32(lds, a2)) ^ lds32(lds, a3 + 128);
+    return xor3(lds32(t.lds, a0), lds32(t.lds, a1 + 128), lds32(t.lds, a2)) ^ lds32(t.lds, a3 + 128);
 }
 
-__device__ __forceinline__ uint32_t op32(const uint8_t *lds, uint32_t o, uint32_t x) {
-    const uint32_t base = kL32Main + o * 512;
+__device__ __forceinline__ uint32_t f32s(Tab32<true> t, uint32_t x, uint32_t, uint32_t) {
+    const uint32_t a0 = (x << 2) & 0x3FCu, a1 = (x >> 6) & 0x3FCu, a2 = (x >> 14) & 0x3FCu, a3 = (x >> 22) & 0x3FCu;
+    return xor3(lds32(t.lds, a0), lds32(t.lds, a1 + 1024), lds32(t.lds, a2 + 2048)) ^ lds32(t.lds, a3 + 3072);
+}
+
+template <bool LIGHT>
+__device__ __forceinline__ uint32_t op32(Tab32<LIGHT> tab, uint32_t o, uint32_t x) {
+    const uint32_t base = (LIGHT ? kL32LightMain : kL32Main) + o * 512;
     uint32_t t[8];
 #pragma unroll
-    for (int h = 0; h < 8; h++) t[h] = lds32(lds, base + h * 64 + (((x >> (4 * h)) & 15u) << 2));
+    for (int h = 0; h < 8; h++) t[h] = lds32(tab.lds, base + h * 64 + (((x >> (4 * h)) & 15u) << 2));
     return xor3(xor3(t[0], t[1], t[2]), xor3(t[3], t[4], t[5]), t[6] ^ t[7]);
 }
 
-template <int LOG2G>
-__device__ __forceinline__ uint32_t combine32(const uint8_t *lds, uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3,
+template <int LOG2G, class TAB>
+__device__ __forceinline__ uint32_t combine32(TAB lds, uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3,
                                               uint32_t gl) {
     uint32_t x = s0 ^ op32(lds, 0, s1);
     const uint32_t y = s2 ^ op32(lds, 0, s3);
@@ -186,23 +205,30 @@ __device__ __forceinline__ uint32_t combine32(const uint8_t *lds, uint32_t s0, u
     return x;
 }
 
+template <bool LIGHT, int BLOCK>
 __device__ void fill_lds32(uint8_t *lds, const crc32_gpu_pack_t *pk) {
     uint32_t *l = reinterpret_cast<uint32_t *>(lds);
-    for (uint32_t d = threadIdx.x; d < 32768u; d += kBlock) {
-        const uint32_t region = d >> 14, e = (d >> 6) & 255u, half = (d >> 5) & 1u;
-        l[d] = pk->main[2 * region + half][e];
+    if constexpr (LIGHT) {
+        const uint32_t *m = &pk->main[0][0];
+        for (uint32_t d = threadIdx.x; d < 1024u; d += BLOCK) l[d] = m[d];
+    } else {
+        for (uint32_t d = threadIdx.x; d < 32768u; d += BLOCK) {
+            const uint32_t region = d >> 14, e = (d >> 6) & 255u, half = (d >> 5) & 1u;
+            l[d] = pk->main[2 * region + half][e];
+        }
     }
     const uint32_t *ops = &pk->ops[0][0][0];
     const uint32_t nops = pk->nops * 128u;
-    for (uint32_t d = threadIdx.x; d < nops; d += kBlock) l[kL32Main / 4 + d] = ops[d];
+    const uint32_t base = (LIGHT ? kL32LightMain : kL32Main) / 4;
+    for (uint32_t d = threadIdx.x; d < nops; d += BLOCK) l[base + d] = ops[d];
 }
 
 // Ring slot j % kRing holds the piece of step j, loaded kRing steps ahead.
 //
 // Aligned fixed-size payload: base 16-B aligned, len = K * 16G, no masking,
 // no pad bytes (tail op is the identity and is skipped).
-template <int LOG2G, bool NT>
-__device__ __forceinline__ uint32_t payload32_aligned(const uint8_t *lds, const uint8_t *p, uint64_t K, uint32_t gl,
+template <int LOG2G, bool NT, class TAB>
+__device__ __forceinline__ uint32_t payload32_aligned(TAB lds, const uint8_t *p, uint64_t K, uint32_t gl,
                                                       uint32_t lc0, uint32_t lc1, uint32_t init) {
     constexpr int G = 1 << LOG2G;
     const uint4 *src = reinterpret_cast<const uint4 *>(p) + gl;
@@ -239,8 +265,8 @@ __device__ __forceinline__ T wave_max(T v) {
 
 // Any alignment, any length (0 included).  Per-lane window; the wave loops to
 // the largest step count of its groups.
-template <int LOG2G, bool NT>
-__device__ __forceinline__ uint32_t payload32_generic(const uint8_t *lds, const crc32_gpu_pack_t *pk,
+template <int LOG2G, bool NT, class TAB>
+__device__ __forceinline__ uint32_t payload32_generic(TAB lds, const crc32_gpu_pack_t *pk,
                                                       const uint8_t *p, uint64_t len, uint32_t gl, uint32_t lc0,
                                                       uint32_t lc1) {
     constexpr int G = 1 << LOG2G;
@@ -304,8 +330,8 @@ __device__ __forceinline__ uint32_t payload32_generic(const uint8_t *lds, const 
 // payload base stays in SGPRs, each lane carries a 32-bit offset (saddr-form
 // global loads), and "does this step touch an edge?" is a scalar test -- only
 // the first/last steps pay for per-lane masking.  Payloads < 2 GiB.
-template <bool NT>
-__device__ __forceinline__ uint32_t payload32_g64(const uint8_t *lds, const crc32_gpu_pack_t *pk, const uint8_t *p,
+template <bool NT, class TAB>
+__device__ __forceinline__ uint32_t payload32_g64(TAB lds, const crc32_gpu_pack_t *pk, const uint8_t *p,
                                                   uint64_t len, uint32_t gl, uint32_t lc0, uint32_t lc1) {
     const uint32_t init = pk->init;
     const uint64_t sa = reinterpret_cast<uint64_t>(p), ea = sa + len;
@@ -393,12 +419,17 @@ __device__ __forceinline__ void emit(const BatchArgs &a, uint64_t p, T v) {
     }
 }
 
-template <int LOG2G, int MODE, bool VERIFY, bool NT>
-__global__ __launch_bounds__(kBlock, 1) void crc32c_batch_kernel(BatchArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kL32Bytes];
+template <bool LIGHT>
+constexpr int kBlk32 = LIGHT ? kLightBlock : kBlock;
+
+template <int LOG2G, int MODE, bool VERIFY, bool NT, bool LIGHT = false>
+__global__ __launch_bounds__(kBlk32<LIGHT>, 1) void crc32c_batch_kernel(BatchArgs a) {
+    constexpr int kWavesPerBlock = kBlk32<LIGHT> / 64;
+    __shared__ __attribute__((aligned(16))) uint8_t lds_raw[LIGHT ? kL32LightBytes : kL32Bytes];
     const crc32_gpu_pack_t *pk = reinterpret_cast<const crc32_gpu_pack_t *>(a.pack);
-    fill_lds32(lds, pk);
+    fill_lds32<LIGHT, kBlk32<LIGHT>>(lds_raw, pk);
     __syncthreads();
+    const Tab32<LIGHT> lds{lds_raw};
 
     constexpr int PPW = 64 >> LOG2G;
     const uint32_t lane = threadIdx.x & 63u;
@@ -809,34 +840,62 @@ struct KLaunch {
     int block, blocks_per_cu;
 };
 
-template <int W, int LOG2G, int MODE, bool VERIFY, bool NT = false>
+template <int W, int LOG2G, int MODE, bool VERIFY, bool NT = false, bool LIGHT = false>
 KLaunch kernel_ptr() {
-    using S = Shape<W, MODE>;
-    if constexpr (W == 32) return {crc32c_batch_kernel<LOG2G, MODE, VERIFY, NT>, S::block, S::blocks_per_cu};
+    using S = Shape<W, MODE, LIGHT>;
+    if constexpr (W == 32) return {crc32c_batch_kernel<LOG2G, MODE, VERIFY, NT, LIGHT>, S::block, S::blocks_per_cu};
     else return {crc64_batch_kernel<LOG2G, MODE, VERIFY, NT>, S::block, S::blocks_per_cu};
 }
 
 template <int W, int LOG2G>
-KLaunch pick_fixed_lg(bool aligned, bool nt) {
+KLaunch pick_fixed_lg(bool aligned, bool nt, bool light) {
+    if constexpr (W == 32) {
+        if (light)
+            return aligned ? kernel_ptr<W, LOG2G, kFixedAligned, false, false, true>()
+                           : kernel_ptr<W, LOG2G, kFixedGeneric, false, false, true>();
+    }
     if (!aligned) return kernel_ptr<W, LOG2G, kFixedGeneric, false>();
     return nt ? kernel_ptr<W, LOG2G, kFixedAligned, false, true>() : kernel_ptr<W, LOG2G, kFixedAligned, false>();
 }
 
 template <int W>
-KLaunch pick_fixed(int log2g, bool aligned, bool nt) {
+KLaunch pick_fixed(int log2g, bool aligned, bool nt, bool light) {
     switch (log2g) {
-        case 0: return pick_fixed_lg<W, 0>(aligned, nt);
-        case 1: return pick_fixed_lg<W, 1>(aligned, nt);
-        case 2: return pick_fixed_lg<W, 2>(aligned, nt);
-        case 3: return pick_fixed_lg<W, 3>(aligned, nt);
-        case 4: return pick_fixed_lg<W, 4>(aligned, nt);
-        case 5: return pick_fixed_lg<W, 5>(aligned, nt);
-        default: return pick_fixed_lg<W, 6>(aligned, nt);
+        case 0: return pick_fixed_lg<W, 0>(aligned, nt, light);
+        case 1: return pick_fixed_lg<W, 1>(aligned, nt, light);
+        case 2: return pick_fixed_lg<W, 2>(aligned, nt, light);
+        case 3: return pick_fixed_lg<W, 3>(aligned, nt, light);
+        case 4: return pick_fixed_lg<W, 4>(aligned, nt, light);
+        case 5: return pick_fixed_lg<W, 5>(aligned, nt, light);
+        default: return pick_fixed_lg<W, 6>(aligned, nt, light);
     }
 }
 
 // Non-temporal payload loads when the batch is far larger than the 256 MiB
 // Infinity Cache (MCHECKSUM_GPU_NT=0/1 overrides).
+// Small batches take the light CRC-32C layout (16 KiB LDS fill, 256-thread
+// workgroups over every CU, 64 lanes per payload): the full layout's 140 KiB
+// fill and 1024-thread workgroups cost ~6-12 us per call there
+// (profiles/r01/latency.json).  MCHECKSUM_GPU_LIGHT=0/1 overrides.
+constexpr uint64_t kLightMaxBytes = 8ull << 20;
+bool use_light(uint64_t batch_bytes, bool known) {
+    const char *env = getenv("MCHECKSUM_GPU_LIGHT");
+    if (env && env[0]) return env[0] == '1';
+    return known && batch_bytes <= kLightMaxBytes;
+}
+
+// Lanes per payload for the light layout: as many as keep K >= kRing whole steps.
+int light_log2g(size_t len) {
+    const char *env = getenv("MCHECKSUM_GPU_LOG2G");
+    if (env && env[0]) {
+        const int v = atoi(env);
+        if (v >= 0 && v <= CRC_GPU_MAX_LOG2G) return v;
+    }
+    int lg = CRC_GPU_MAX_LOG2G;
+    while (lg > 0 && ((size_t)16 << lg) * kRing > len) lg--;
+    return lg;
+}
+
 bool use_nt(uint64_t batch_bytes) {
     const char *env = getenv("MCHECKSUM_GPU_NT");
     if (env && env[0]) return env[0] == '1';
@@ -899,13 +958,38 @@ int do_offsets(const char *method, const void *base, const uint64_t *offsets, si
     // The offsets table stays on the device, so size the batch by its count:
     // 8192+ payloads of the C4 mix are ~270 MB and up.
     const bool nt = use_nt(count >= 8192 ? (1ull << 40) : 0);
-    if (width == 32)
+    // small offsets batches (<= 1024 payloads: a receive queue's worth of RPCs)
+    // take the light layout
+    const bool light = width == 32 && use_light(count <= 1024 ? 0 : ~0ull, true);
+    if (width == 32 && light)
+        k = verify ? kernel_ptr<32, 6, kOffsets, true, false, true>() : kernel_ptr<32, 6, kOffsets, false, false, true>();
+    else if (width == 32)
         k = verify ? (nt ? kernel_ptr<32, 6, kOffsets, true, true>() : kernel_ptr<32, 6, kOffsets, true>())
                    : (nt ? kernel_ptr<32, 6, kOffsets, false, true>() : kernel_ptr<32, 6, kOffsets, false>());
     else
         k = verify ? (nt ? kernel_ptr<64, 6, kOffsets, true, true>() : kernel_ptr<64, 6, kOffsets, true>())
                    : (nt ? kernel_ptr<64, 6, kOffsets, false, true>() : kernel_ptr<64, 6, kOffsets, false>());
     return launch(k, a, grid_for(c, count, k), stream);
+}
+
+int launch_fixed(DevCtx *c, const void *pack, int width, int lg, const void *dev_base, size_t stride, size_t len,
+                 size_t count, void *dev_out, void *stream, bool light) {
+    const uint64_t step = 16ull << lg;
+    // The aligned path needs whole steps and K = len/step a multiple of the
+    // load ring depth; everything else takes the generic path.
+    const bool aligned = ((uintptr_t)dev_base % 16 == 0) && (stride % 16 == 0 || count == 1) &&
+                         len >= step * kRing && (len % (step * kRing) == 0) && !getenv("MCHECKSUM_GPU_FORCE_GENERIC");
+    BatchArgs a{};
+    a.base = (const uint8_t *)dev_base;
+    a.stride = stride;
+    a.len = len;
+    a.count = count;
+    a.out = dev_out;
+    a.pack = pack;
+    const bool nt = !light && use_nt((uint64_t)len * count);
+    const KLaunch k = width == 32 ? pick_fixed<32>(lg, aligned, nt, light) : pick_fixed<64>(lg, aligned, nt, false);
+    const uint64_t ppw = 64u >> lg;
+    return launch(k, a, grid_for(c, (count + ppw - 1) / ppw, k), stream);
 }
 
 }  // namespace
@@ -944,27 +1028,23 @@ int mchecksum_gpu_checksum_fixed(const char *hash_method, const void *dev_base, 
     if (count && (!dev_base || !dev_out)) return set_err(MCHECKSUM_GPU_EINVAL, "NULL pointer argument%s%d");
     if (count > 1 && stride < len) return set_err(MCHECKSUM_GPU_EINVAL, "stride smaller than len%s%d");
     if (!mchecksum_gpu_available()) return set_err(MCHECKSUM_GPU_ENODEV, "no HIP device%s%d");
-    const int lg = choose_log2g(len);
     int width = 0;
+    if (gpu_model(hash_method, &width) >= 0 && width == 32 && use_light((uint64_t)len * count, true)) {
+        const int lg = light_log2g(len);
+        DevCtx *c = nullptr;
+        const void *pack = nullptr;
+        int rc = prologue(hash_method, lg, &width, &c, &pack);
+        if (rc) return rc;
+        if (count == 0) return MCHECKSUM_GPU_OK;
+        return launch_fixed(c, pack, width, lg, dev_base, stride, len, count, dev_out, stream, true);
+    }
+    const int lg = choose_log2g(len);
     DevCtx *c = nullptr;
     const void *pack = nullptr;
     int rc = prologue(hash_method, lg, &width, &c, &pack);
     if (rc) return rc;
     if (count == 0) return MCHECKSUM_GPU_OK;
-    const uint64_t step = 16ull << lg;
-    const bool aligned = ((uintptr_t)dev_base % 16 == 0) && (stride % 16 == 0 || count == 1) && len >= step &&
-                         (len % step == 0) && !getenv("MCHECKSUM_GPU_FORCE_GENERIC");
-    BatchArgs a{};
-    a.base = (const uint8_t *)dev_base;
-    a.stride = stride;
-    a.len = len;
-    a.count = count;
-    a.out = dev_out;
-    a.pack = pack;
-    const bool nt = use_nt((uint64_t)len * count);
-    const KLaunch k = width == 32 ? pick_fixed<32>(lg, aligned, nt) : pick_fixed<64>(lg, aligned, nt);
-    const uint64_t ppw = 64u >> lg;
-    return launch(k, a, grid_for(c, (count + ppw - 1) / ppw, k), stream);
+    return launch_fixed(c, pack, width, lg, dev_base, stride, len, count, dev_out, stream, false);
 }
 
 int mchecksum_gpu_checksum_offsets(const char *hash_method, const void *dev_base, const uint64_t *dev_offsets,

@@ -37,8 +37,17 @@ def _force_log2g(lg):
 @pytest.fixture(autouse=True)
 def _clean_env():
     yield
-    os.environ.pop("MCHECKSUM_GPU_LOG2G", None)
-    os.environ.pop("MCHECKSUM_GPU_FORCE_GENERIC", None)
+    for k in ("MCHECKSUM_GPU_LOG2G", "MCHECKSUM_GPU_FORCE_GENERIC", "MCHECKSUM_GPU_LIGHT"):
+        os.environ.pop(k, None)
+
+
+@pytest.fixture(params=["full", "light"])
+def layout(request):
+    """Both CRC-32C table layouts: the 32x-replicated throughput layout and the
+    light small-batch layout (MCHECKSUM_GPU_LIGHT forces the choice)."""
+    os.environ["MCHECKSUM_GPU_LIGHT"] = "1" if request.param == "light" else "0"
+    yield request.param
+    os.environ.pop("MCHECKSUM_GPU_LIGHT", None)
 
 
 def test_selfcheck_small_known_answers(gpu, oracle_mod):
@@ -62,7 +71,7 @@ def test_selfcheck_small_known_answers(gpu, oracle_mod):
     (4096, 4096), (65536, 65536), (1024, 1024), (256, 256), (16, 16),
     (4096, 4100), (1000, 1000), (3, 7), (0, 16), (1, 1), (17, 33), (65537, 65552), (4095, 4096), (100000, 100003),
 ])
-def test_fixed_every_lane_width(gpu, oracle_mod, method, length, stride):
+def test_fixed_every_lane_width(gpu, oracle_mod, method, length, stride, layout):
     import torch
     count = 67
     nbytes = (count - 1) * stride + length
@@ -78,7 +87,7 @@ def test_fixed_every_lane_width(gpu, oracle_mod, method, length, stride):
 
 
 @pytest.mark.parametrize("method", METHODS)
-def test_fixed_unaligned_base_generic_path(gpu, oracle_mod, method):
+def test_fixed_unaligned_base_generic_path(gpu, oracle_mod, method, layout):
     import torch
     length, count = 4096, 40
     host = oracle_mod.splitmix_bytes(count * length + 64, SEED_C2)
@@ -96,7 +105,7 @@ def test_fixed_unaligned_base_generic_path(gpu, oracle_mod, method):
 
 
 @pytest.mark.parametrize("method", METHODS)
-def test_offsets_varlen_c4_layout(gpu, oracle_mod, method):
+def test_offsets_varlen_c4_layout(gpu, oracle_mod, method, layout):
     import torch
     count = 3000  # C4 shape, scaled: U[64 B, 64 KiB] packed at byte granularity
     off = oracle_mod.varlen_offsets(SEED_C4, count)
@@ -110,7 +119,7 @@ def test_offsets_varlen_c4_layout(gpu, oracle_mod, method):
 
 
 @pytest.mark.parametrize("method", METHODS)
-def test_offsets_edge_cases(gpu, oracle_mod, method):
+def test_offsets_edge_cases(gpu, oracle_mod, method, layout):
     import torch
     rng = np.random.default_rng(7)
     lens = [0, 0, 1, 2, 3, 4, 5, 7, 8, 9, 15, 16, 17, 0, 31, 32, 33, 63, 64, 65, 1023, 1024, 1025, 0]
@@ -143,7 +152,7 @@ def test_all_zero_and_all_ones_batches(gpu, oracle_mod, method):
         assert len(set(got.tolist())) == 1
 
 
-def test_verify_detects_single_bit_corruption(gpu, oracle_mod):
+def test_verify_detects_single_bit_corruption(gpu, oracle_mod, layout):
     import torch
     count = 500
     off = oracle_mod.varlen_offsets(SEED_C4 ^ 1, count)

@@ -45,7 +45,9 @@ def _batch(rng, n):
     return b"".join(msgs), off, crcs
 
 
-def test_verify_messages_in_place(gpu, oracle_mod):
+@pytest.mark.parametrize("light", ["0", "1"])
+def test_verify_messages_in_place(gpu, oracle_mod, light, monkeypatch):
+    monkeypatch.setenv("MCHECKSUM_GPU_LIGHT", light)
     import torch
     rng = np.random.default_rng(2024)
     buf, off, crcs = _batch(rng, 700)

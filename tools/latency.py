@@ -15,40 +15,42 @@ def main():
     G.prepare("crc32c")
     big = torch.empty(16384 * length + 64, dtype=torch.uint8, device="cuda")
     G.fill_splitmix(big, 1)
-    for count in (1, 8, 64, 256, 1024, 4096, 16384):
-        out = torch.empty(count, dtype=torch.int32, device="cuda")
-        f = lambda: G.checksum_fixed("crc32c", big, length, count=count, out=out)
-        for _ in range(5):
-            f()
-        torch.cuda.synchronize()
-        s = torch.cuda.current_stream()
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(50)]
-        for a, b in ev:
-            a.record(s); f(); b.record(s)
-        torch.cuda.synchronize()
-        dev_us = float(np.median([a.elapsed_time(b) for a, b in ev])) * 1e3
-        n = 200
-        t0 = time.perf_counter()
-        for _ in range(n):
-            f()
-        torch.cuda.synchronize()
-        eager_us = (time.perf_counter() - t0) / n * 1e6
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            f()
-        ref = out.clone()
-        g.replay(); torch.cuda.synchronize()
-        same = bool(torch.equal(ref, out))
-        t0 = time.perf_counter()
-        for _ in range(n):
-            g.replay()
-        torch.cuda.synchronize()
-        graph_us = (time.perf_counter() - t0) / n * 1e6
-        r = {"payloads": count, "bytes": count * length, "device_us": round(dev_us, 2),
-             "eager_wall_us_per_call": round(eager_us, 2), "graph_wall_us_per_replay": round(graph_us, 2),
-             "graph_result_identical": same, "GBps_device": round(count * length / dev_us / 1e3, 1)}
-        print(json.dumps(r), flush=True)
-        res.append(r)
+    for light in ("0", "1"):
+      os.environ["MCHECKSUM_GPU_LIGHT"] = light
+      for count in (1, 8, 64, 256, 1024, 4096):
+          out = torch.empty(count, dtype=torch.int32, device="cuda")
+          f = lambda: G.checksum_fixed("crc32c", big, length, count=count, out=out)
+          for _ in range(5):
+              f()
+          torch.cuda.synchronize()
+          s = torch.cuda.current_stream()
+          ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(50)]
+          for a, b in ev:
+              a.record(s); f(); b.record(s)
+          torch.cuda.synchronize()
+          dev_us = float(np.median([a.elapsed_time(b) for a, b in ev])) * 1e3
+          n = 200
+          t0 = time.perf_counter()
+          for _ in range(n):
+              f()
+          torch.cuda.synchronize()
+          eager_us = (time.perf_counter() - t0) / n * 1e6
+          g = torch.cuda.CUDAGraph()
+          with torch.cuda.graph(g):
+              f()
+          ref = out.clone()
+          g.replay(); torch.cuda.synchronize()
+          same = bool(torch.equal(ref, out))
+          t0 = time.perf_counter()
+          for _ in range(n):
+              g.replay()
+          torch.cuda.synchronize()
+          graph_us = (time.perf_counter() - t0) / n * 1e6
+          r = {"light": light, "payloads": count, "bytes": count * length, "device_us": round(dev_us, 2),
+               "eager_wall_us_per_call": round(eager_us, 2), "graph_wall_us_per_replay": round(graph_us, 2),
+               "graph_result_identical": same, "GBps_device": round(count * length / dev_us / 1e3, 1)}
+          print(json.dumps(r), flush=True)
+          res.append(r)
     json.dump(res, open(os.path.join(ROOT, "gpurun_out", "latency.json"), "w"), indent=1)
 
 if __name__ == "__main__":
