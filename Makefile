@@ -64,7 +64,7 @@ clean:
 
 # A/B variants of the batch kernels (tools/ab_variants.py).  Each is a full
 # libmchecksum built with different tuning macros.
-VARIANTS := base:-DMCK_RING=4 ring6:-DMCK_RING=6 ring8:-DMCK_RING=8
+VARIANTS := base:-DMCK_RING=4 sdwa0:-DMCK_SDWA64=0 split1:-DMCK_CRC64_SPLIT=1 ring6:-DMCK_RING=6
 variants: $(COBJS) | $(BUILD)
 	mkdir -p $(BUILD)/variants
 	@for v in $(VARIANTS); do n=$${v%%:*}; f=$$(echo $${v#*:} | tr , " "); \
@@ -73,3 +73,12 @@ variants: $(COBJS) | $(BUILD)
 	  $(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $(BUILD)/variants/libmchecksum_$$n.so $(COBJS) $(BUILD)/variants/gpu_$$n.o -lpthread || exit 1; \
 	done
 .PHONY: variants
+
+# The committed kernel source at $(PREV) as variant "prev" (A/B against the last commit).
+PREV ?= HEAD
+prev: $(COBJS) | $(BUILD)
+	mkdir -p $(BUILD)/variants
+	git show $(PREV):mercury_amd/csrc/mchecksum_gpu.hip > $(BUILD)/variants/prev_gpu.hip
+	$(HIPCC) $(HIPFLAGS) $(INC) -I$(CSRC) -c $(BUILD)/variants/prev_gpu.hip -o $(BUILD)/variants/gpu_prev.o
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $(BUILD)/variants/libmchecksum_prev.so $(COBJS) $(BUILD)/variants/gpu_prev.o -lpthread
+.PHONY: variants prev

@@ -75,26 +75,38 @@ template <bool LIGHT>
 struct Tab32 {
     const uint8_t *lds;
 };
-// CRC-64 LDS map: [0,64K) main nibble tables x32 copies; then op nibble tables.
-constexpr uint32_t kL64Main = 65536;
+// CRC-64 LDS map.  A 64-bit state is looked up by nibble: the 8 low-nibble
+// tables are replicated 32x (entry v at v*256 B, lane copy at (lane%32)*8 B;
+// the address is one v_perm of the masked nibble and the lane byte), the 8
+// high-nibble tables are NOT replicated: entry v sits at v*16 B, so the masked
+// byte (v << 4) is its own address and the 16 entries fall on 16 distinct bank
+// pairs of ds_read_b64 (lanes that share an entry broadcast) -- conflict-free
+// without copies.  Then the combine operators (nibble tables, 2 KiB each).
+constexpr uint32_t kL64Hi = 32768;
+constexpr uint32_t kL64Main = kL64Hi + 8 * 256;
 constexpr uint32_t kL64Bytes = kL64Main + CRC64_NOPS_MAX * 2048;
-// CRC-64 over large aligned payloads is latency-bound at one workgroup per CU
-// (SQ_WAIT_INST_ANY 40% of wave time).  Its "split" launch shape keeps only the
-// 64 KiB main tables in LDS and reads the combine operators (touched once per
-// payload) from global memory, so two workgroups of MCK_BLOCK64 threads fit a
-// CU.  Variable-length batches keep the operators in LDS (many combines).
+// CRC-64 is VALU-bound (the table XOR tree); two 1024-thread workgroups per CU
+// (8 waves/SIMD, 80 KiB LDS each) hide the LDS latency.  MCK_CRC64_SPLIT=1
+// reads the combine operators (touched once per payload) from global memory
+// instead of LDS on the aligned path.
 #ifndef MCK_CRC64_SPLIT
-#define MCK_CRC64_SPLIT 1
+#define MCK_CRC64_SPLIT 0
 #endif
 #ifndef MCK_BLOCK64
 #define MCK_BLOCK64 1024
+#endif
+// Fold the next data word into the table-XOR tree (its 17th input slot is
+// free) and run the aligned step loop without per-step bounds tests.
+#ifndef MCK_LA64
+#define MCK_LA64 1
 #endif
 
 template <int W, int MODE, bool LIGHT = false>
 struct Shape {
     static constexpr bool ops_global = W == 64 && MODE == 0 && MCK_CRC64_SPLIT;  // 0 = kFixedAligned
-    static constexpr int block = LIGHT ? kLightBlock : ops_global ? MCK_BLOCK64 : kBlock;
-    static constexpr int blocks_per_cu = LIGHT ? 8 : ops_global ? 2 : 1;
+    static constexpr bool two = W == 64 && MODE == 0;
+    static constexpr int block = LIGHT ? kLightBlock : two ? MCK_BLOCK64 : kBlock;
+    static constexpr int blocks_per_cu = LIGHT ? 8 : two ? 2 : 1;
     static constexpr uint32_t lds64_bytes = ops_global ? kL64Main : kL64Bytes;
 };
 // single-argument aliases (a comma inside __launch_bounds__ splits the macro)
@@ -489,21 +501,84 @@ __device__ __forceinline__ uint64_t xor17(const uint64_t *r, uint64_t extra) {
     return xor3_64(xor3_64(r[15], extra, a), xor3_64(b, c, d), e);
 }
 
-// Z^(16G)(x) ^ next from 16 nibble tables (next = 0 in the step loop); table 2p+h at (2p+h)*4 KiB, entry
-// v at v*256 B, lane copy at (lane%32)*8 B.
-__device__ __forceinline__ uint64_t f64x(const uint8_t *lds, uint64_t x, uint64_t next, uint32_t lc) {
-    const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
-    const uint32_t n0 = xl & 0x0F0F0F0Fu, n1 = (xl >> 4) & 0x0F0F0F0Fu;
-    const uint32_t n2 = xh & 0x0F0F0F0Fu, n3 = (xh >> 4) & 0x0F0F0F0Fu;
-    uint64_t r[16];
-#pragma unroll
-    for (int b = 0; b < 4; b++) {
-        const uint32_t sel = 0x0C0C0400u | ((uint32_t)b << 8);
-        r[4 * b + 0] = lds64(lds, __builtin_amdgcn_perm(n0, lc, sel) + (2 * b + 0) * 4096);
-        r[4 * b + 1] = lds64(lds, __builtin_amdgcn_perm(n1, lc, sel) + (2 * b + 1) * 4096);
-        r[4 * b + 2] = lds64(lds, __builtin_amdgcn_perm(n2, lc, sel) + (2 * (b + 4) + 0) * 4096);
-        r[4 * b + 3] = lds64(lds, __builtin_amdgcn_perm(n3, lc, sel) + (2 * (b + 4) + 1) * 4096);
+#ifndef MCK_SDWA64
+#define MCK_SDWA64 1
+#endif
+
+// Per-lane lookup address registers of f64x.  With SDWA (gfx9 sub-dword
+// operands) one v_and_b32_sdwa both extracts a nibble of byte b and places it:
+// the high nibble as (byte & 0xF0) -- its own address -- and the low nibble
+// into byte 1 of a persistent register whose byte 0 holds the lane copy offset
+// (dst_unused:UNUSED_PRESERVE keeps it), so a lookup costs one VALU op and no
+// separate masking.
+struct Lane64 {
+    uint32_t lc;
+    uint32_t al[4];
+};
+__device__ __forceinline__ Lane64 lane64(uint32_t lc) { return Lane64{lc, {lc, lc, lc, lc}}; }
+
+#define MCK_SDWA_HI(B)                                                                              \
+    __device__ __forceinline__ uint32_t sdwa_hi##B(uint32_t x) {                                    \
+        uint32_t r;                                                                                 \
+        asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD "         \
+            "src1_sel:BYTE_" #B : "=v"(r) : "s"(0xF0u), "v"(x));                                    \
+        return r;                                                                                   \
+    }                                                                                               \
+    __device__ __forceinline__ void sdwa_lo##B(uint32_t &a, uint32_t x) {                           \
+        asm("v_and_b32_sdwa %0, %1, %2 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD "   \
+            "src1_sel:BYTE_" #B : "+v"(a) : "s"(0x0Fu), "v"(x));                                    \
     }
+MCK_SDWA_HI(0)
+MCK_SDWA_HI(1)
+MCK_SDWA_HI(2)
+MCK_SDWA_HI(3)
+#undef MCK_SDWA_HI
+
+template <int B>
+__device__ __forceinline__ uint32_t sdwa_hi(uint32_t x) {
+    if constexpr (B == 0) return sdwa_hi0(x);
+    else if constexpr (B == 1) return sdwa_hi1(x);
+    else if constexpr (B == 2) return sdwa_hi2(x);
+    else return sdwa_hi3(x);
+}
+template <int B>
+__device__ __forceinline__ void sdwa_lo(uint32_t &a, uint32_t x) {
+    if constexpr (B == 0) sdwa_lo0(a, x);
+    else if constexpr (B == 1) sdwa_lo1(a, x);
+    else if constexpr (B == 2) sdwa_lo2(a, x);
+    else sdwa_lo3(a, x);
+}
+
+template <int B>
+__device__ __forceinline__ void f64x_byte(const uint8_t *lds, uint32_t xl, uint32_t xh, Lane64 &ln, uint64_t *r) {
+#if MCK_SDWA64
+    sdwa_lo<B>(ln.al[B], xl);
+    r[4 * B + 0] = lds64(lds, ln.al[B] + B * 4096);
+    r[4 * B + 1] = lds64(lds, sdwa_hi<B>(xl) + kL64Hi + B * 256);
+    sdwa_lo<B>(ln.al[B], xh);
+    r[4 * B + 2] = lds64(lds, ln.al[B] + (B + 4) * 4096);
+    r[4 * B + 3] = lds64(lds, sdwa_hi<B>(xh) + kL64Hi + (B + 4) * 256);
+#else
+    const uint32_t sl = 0x0C0C0400u | ((uint32_t)B << 8);  // byte B -> address byte 1, lane byte -> 0
+    const uint32_t sh = 0x0C0C0C04u | (uint32_t)B;         // byte B -> address byte 0
+    const uint32_t l0 = xl & 0x0F0F0F0Fu, h0 = xl & 0xF0F0F0F0u;
+    const uint32_t l1 = xh & 0x0F0F0F0Fu, h1 = xh & 0xF0F0F0F0u;
+    r[4 * B + 0] = lds64(lds, __builtin_amdgcn_perm(l0, ln.lc, sl) + B * 4096);
+    r[4 * B + 1] = lds64(lds, __builtin_amdgcn_perm(h0, h0, sh) + kL64Hi + B * 256);
+    r[4 * B + 2] = lds64(lds, __builtin_amdgcn_perm(l1, ln.lc, sl) + (B + 4) * 4096);
+    r[4 * B + 3] = lds64(lds, __builtin_amdgcn_perm(h1, h1, sh) + kL64Hi + (B + 4) * 256);
+#endif
+}
+
+// Z^(16G)(x) ^ next from the 16 nibble tables (LDS map above): one VALU op per
+// lookup to form its address, 8 v_bitop3 per 32-bit half for the XOR tree.
+__device__ __forceinline__ uint64_t f64x(const uint8_t *lds, uint64_t x, uint64_t next, Lane64 &ln) {
+    const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
+    uint64_t r[16];
+    f64x_byte<0>(lds, xl, xh, ln, r);
+    f64x_byte<1>(lds, xl, xh, ln, r);
+    f64x_byte<2>(lds, xl, xh, ln, r);
+    f64x_byte<3>(lds, xl, xh, ln, r);
     return xor17(r, next);
 }
 
@@ -539,7 +614,9 @@ __device__ __forceinline__ uint64_t combine64(const uint8_t *lds, const crc64_gp
 template <int BLOCK, bool OG>
 __device__ void fill_lds64(uint8_t *lds, const crc64_gpu_pack_t *pk) {
     uint64_t *l = reinterpret_cast<uint64_t *>(lds);
-    for (uint32_t d = threadIdx.x; d < 8192u; d += BLOCK) l[d] = pk->main[d >> 9][(d >> 5) & 15u];
+    // low-nibble tables (main[2p]), 32 copies; high-nibble tables (main[2p+1]) at 16-B entry stride
+    for (uint32_t d = threadIdx.x; d < 4096u; d += BLOCK) l[d] = pk->main[2 * (d >> 9)][(d >> 5) & 15u];
+    for (uint32_t d = threadIdx.x; d < 128u; d += BLOCK) l[kL64Hi / 8 + (d >> 4) * 32 + (d & 15u) * 2] = pk->main[2 * (d >> 4) + 1][d & 15u];
     if constexpr (!OG) {
         const uint64_t *ops = &pk->ops[0][0][0];
         const uint32_t nops = pk->nops * 256u;
@@ -552,25 +629,53 @@ __device__ __forceinline__ uint64_t hi64(uint4 v) { return (uint64_t)v.w << 32 |
 
 template <int LOG2G, bool NT, bool OG>
 __device__ __forceinline__ uint64_t payload64_aligned(const uint8_t *lds, const crc64_gpu_pack_t *pk, const uint8_t *p,
-                                                      uint64_t K, uint32_t gl, uint32_t lc, uint64_t init) {
+                                                      uint32_t K, uint32_t gl, uint32_t lc, uint64_t init) {
     constexpr int G = 1 << LOG2G;
+    constexpr int R = kRing;
+    Lane64 ln = lane64(lc);
     const uint4 *src = reinterpret_cast<const uint4 *>(p) + gl;
-    uint4 ring[kRing];
+    uint4 ring[R];
 #pragma unroll
-    for (int u = 0; u < kRing; u++) ring[u] = (uint64_t)u < K ? ld16<NT>(src + (uint64_t)u * G) : make_uint4(0, 0, 0, 0);
-    uint64_t x0 = gl == 0 ? init : 0ull, x1 = 0;
-    for (uint64_t k = 0; k < K; k += kRing) {
+    for (int u = 0; u < R; u++) ring[u] = (uint32_t)u < K ? ld16<NT>(src + (uint64_t)u * G) : make_uint4(0, 0, 0, 0);
+#if MCK_LA64
+    // x holds state ^ (the data word of the step about to run)
+    uint64_t x0 = (gl == 0 ? init : 0ull) ^ lo64(ring[0]), x1 = hi64(ring[0]);
+    uint32_t k = 0;
+    for (; k + 2 * R <= K; k += R) {  // every load and look-ahead in range
 #pragma unroll
-        for (int u = 0; u < kRing; u++) {
-            const uint4 v = ring[u];
-            const uint64_t kn = k + u + kRing;
-            if (kn < K) ring[u] = ld16<NT>(src + kn * G);
+        for (int u = 0; u < R; u++) {
+            ring[u] = ld16<NT>(src + (uint64_t)(k + u + R) * G);
+            const uint4 nx = ring[(u + 1) % R];
+            x0 = f64x(lds, x0, lo64(nx), ln);
+            x1 = f64x(lds, x1, hi64(nx), ln);
+        }
+    }
+    for (; k < K; k += R) {
+#pragma unroll
+        for (int u = 0; u < R; u++) {
+            if (k + u + R < K) ring[u] = ld16<NT>(src + (uint64_t)(k + u + R) * G);
             if (k + u < K) {
-                x0 = f64x(lds, x0 ^ lo64(v), 0, lc);
-                x1 = f64x(lds, x1 ^ hi64(v), 0, lc);
+                const uint4 nx = k + u + 1 < K ? ring[(u + 1) % R] : make_uint4(0, 0, 0, 0);
+                x0 = f64x(lds, x0, lo64(nx), ln);
+                x1 = f64x(lds, x1, hi64(nx), ln);
             }
         }
     }
+#else
+    uint64_t x0 = gl == 0 ? init : 0ull, x1 = 0;
+    for (uint32_t k = 0; k < K; k += R) {
+#pragma unroll
+        for (int u = 0; u < R; u++) {
+            const uint4 v = ring[u];
+            const uint32_t kn = k + u + R;
+            if (kn < K) ring[u] = ld16<NT>(src + (uint64_t)kn * G);
+            if (k + u < K) {
+                x0 = f64x(lds, x0 ^ lo64(v), 0, ln);
+                x1 = f64x(lds, x1 ^ hi64(v), 0, ln);
+            }
+        }
+    }
+#endif
     return combine64<LOG2G, OG>(lds, pk, x0, x1, gl);
 }
 
@@ -612,6 +717,7 @@ __device__ __forceinline__ uint64_t payload64_generic(const uint8_t *lds, const 
 #pragma unroll
     for (int u = 0; u < kRing; u++) ring[u] = fetch(u);
     uint64_t x0 = 0, x1 = 0;
+    Lane64 ln = lane64(lc);
     for (int64_t k = 0; k < kmax; k += kRing) {
 #pragma unroll
         for (int u = 0; u < kRing; u++) {
@@ -621,8 +727,8 @@ __device__ __forceinline__ uint64_t payload64_generic(const uint8_t *lds, const 
             if (j < K) {
                 uint64_t w0, w1;
                 prep(j, raw, &w0, &w1);
-                x0 = f64x(lds, x0 ^ w0, 0, lc);
-                x1 = f64x(lds, x1 ^ w1, 0, lc);
+                x0 = f64x(lds, x0 ^ w0, 0, ln);
+                x1 = f64x(lds, x1 ^ w1, 0, ln);
             }
         }
     }
@@ -658,6 +764,7 @@ __device__ __forceinline__ uint64_t payload64_g64(const uint8_t *lds, const crc6
     };
 
     uint64_t x0 = 0, x1 = 0;
+    Lane64 ln = lane64(lc);
     uint4 ring[kRingOff];
 #pragma unroll
     for (int u = 0; u < kRingOff; u++) ring[u] = fetch(u);
@@ -674,8 +781,8 @@ __device__ __forceinline__ uint64_t payload64_g64(const uint8_t *lds, const crc6
                     w0 = mck_mask64(w0, lo, ilen, init);
                     w1 = mck_mask64(w1, lo + 8, ilen, init);
                 }
-                x0 = f64x(lds, x0 ^ w0, 0, lc);
-                x1 = f64x(lds, x1 ^ w1, 0, lc);
+                x0 = f64x(lds, x0 ^ w0, 0, ln);
+                x1 = f64x(lds, x1 ^ w1, 0, ln);
             }
         }
     }
@@ -720,7 +827,7 @@ __global__ __launch_bounds__(kBlk64<MODE>, kWpe64<MODE>) void crc64_batch_kernel
         const uint64_t pc = act ? p : a.count - 1;
         uint64_t x;
         if (MODE == kFixedAligned)
-            x = payload64_aligned<LOG2G, NT, S::ops_global>(lds, pk, a.base + pc * a.stride, a.len >> (4 + LOG2G), gl, lc, pk->init);
+            x = payload64_aligned<LOG2G, NT, S::ops_global>(lds, pk, a.base + pc * a.stride, (uint32_t)(a.len >> (4 + LOG2G)), gl, lc, pk->init);
         else
             x = payload64_generic<LOG2G, NT>(lds, pk, a.base + pc * a.stride, a.len, gl, lc);
         if (act && gl == 0) emit<uint64_t, VERIFY>(a, p, x ^ xorout);
@@ -978,7 +1085,7 @@ int launch_fixed(DevCtx *c, const void *pack, int width, int lg, const void *dev
     // The aligned path needs whole steps and K = len/step a multiple of the
     // load ring depth; everything else takes the generic path.
     const bool aligned = ((uintptr_t)dev_base % 16 == 0) && (stride % 16 == 0 || count == 1) &&
-                         len >= step * kRing && (len % (step * kRing) == 0) && !getenv("MCHECKSUM_GPU_FORCE_GENERIC");
+                         len >= step * kRing && (len % (step * kRing) == 0) && (len >> (4 + lg)) < (1ull << 31) && !getenv("MCHECKSUM_GPU_FORCE_GENERIC");
     BatchArgs a{};
     a.base = (const uint8_t *)dev_base;
     a.stride = stride;
