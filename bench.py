@@ -93,8 +93,8 @@ def main():
         payload_bytes = nbytes
         run = lambda out: G.checksum_fixed(method, data, length, count=count, out=out)  # noqa: E731
     else:
-        from oracle import oracle as O  # layout table only (host offsets), not a checksum
-        offsets_host = O.varlen_offsets(seed ^ rank, count)
+        from mercury_amd.workload import varlen_offsets
+        offsets_host = varlen_offsets(seed ^ rank, count)
         payload_bytes = int(offsets_host[-1])
         data = torch.empty(payload_bytes + 64, dtype=torch.uint8, device=dev)
         G.fill_splitmix(data, seed ^ rank)
@@ -129,32 +129,14 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall_max, kern_ms_max = float(t[0]), float(t[1])
 
-    # ---- parity on the gathered result (outside the timed region) --------
+    # ---- gathered result (outside the timed region) ----------------------
     crcs = out
     if world > 1:
         mine = out.to(coll_dev)
         gathered = [torch.empty_like(mine) for _ in range(world)]
         dist.all_gather(gathered, mine)
         crcs = torch.cat(gathered)
-    parity = "unchecked"
-    if rank == 0:
-        from oracle import oracle as O
-        got = G.as_unsigned(crcs)
-        rng = np.random.default_rng(1234)
-        n_tot = count * world
-        idx = np.unique(np.concatenate([[0, n_tot - 1], rng.integers(0, n_tot, args.parity_samples)]))
-        bad = 0
-        for gi in idx:
-            r, i = divmod(int(gi), count)
-            if layout == "fixed":
-                want = O.splitmix_batch_fixed(method, seed, length, length, int(gi), 1)[0]
-            else:
-                if r != 0:
-                    continue  # other ranks' varlen shards use their own seed; rank 0 checks its own
-                lo, hi = int(offsets_host[i]), int(offsets_host[i + 1])
-                want = O.crc(method, data[lo:hi].cpu().numpy())
-            bad += int(got[gi] != want)
-        parity = f"bit-exact ({len(idx)} sampled payloads vs oracle)" if bad == 0 else f"MISMATCH {bad}/{len(idx)}"
+    got = G.as_unsigned(crcs) if rank == 0 else None
 
     total_bytes = payload_bytes * world * args.steps  # every rank checksummed its shard once per step
     gib_s = total_bytes / wall_max / 2**30
@@ -193,10 +175,17 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel_ms": round(kern_ms_max, 4), "algorithmic_bytes_per_launch": alg_bytes},
-            "parity": parity,
         }
-        if world == 1 and not args.no_cpu_baseline and layout == "fixed":
-            result["cpu_baseline"] = cpu_baseline(method, seed, length, args.cpu_seconds)
+        if world == 1 and not args.no_cpu_baseline:
+            # the only leg that runs the oracle: timed on a bounded sample, and
+            # the checker of the GPU's values (that sample + random payloads)
+            result["cpu_baseline"], result["parity"] = cpu_baseline(
+                method, seed, length, offsets_host, got, args.cpu_seconds, args.parity_samples)
+        elif world > 1:
+            result["parity"] = cross_rank_check(G, method, seed, length, offsets_host, got, count, world, dev,
+                                                args.parity_samples)
+        else:
+            result["parity"] = "unchecked (--no-cpu-baseline)"
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.barrier()
@@ -247,27 +236,89 @@ def bench_c1(args):
     return res
 
 
-def cpu_baseline(method, seed, length, budget_s):
-    """Oracle (CPU restatement of mchecksum) on this host's cores over a bounded
-    sample of the same workload: the reference's own mchecksum is absent from
-    the reference tree, so kind = "port"."""
+def cpu_baseline(method, seed, length, offsets_host, got, budget_s, samples):
+    """The CPU leg (N=1, rank 0): the oracle (CPU restatement of mchecksum --
+    the reference's own mchecksum is absent, so kind = "port") timed on this
+    host's cores over a bounded sample of the same workload (the first n
+    payloads), whose CRCs then check the GPU's values for those payloads; plus
+    `samples` random payloads from the whole batch."""
     from oracle import oracle as O
     threads = max(1, min(16, os.cpu_count() or 1))
-    n = 4096 if length <= 65536 else 256
-    host = O.splitmix_bytes(n * length, seed)
     variant = "sse42" if method == "crc32c" else "table"
-    O.batch_fixed(method, host, length, length, 64, variant=variant, nthreads=threads)  # warm
+    if offsets_host is None:
+        n = 4096 if length <= 65536 else 256
+        host = O.splitmix_bytes(n * length, seed)
+        run = lambda k: O.batch_fixed(method, host, length, length, k, variant=variant, nthreads=threads)  # noqa: E731
+        sample_bytes = n * length
+        what = f"{n} x {length} B"
+    else:
+        n = int(np.searchsorted(offsets_host, np.uint64(256 << 20)))  # ~256 MiB of whole payloads
+        host = O.splitmix_bytes(int(offsets_host[n]), seed)
+        sub = np.ascontiguousarray(offsets_host[:n + 1])
+        run = lambda k: O.batch_offsets(method, host, sub[:k + 1], variant=variant, nthreads=threads)  # noqa: E731
+        sample_bytes = int(offsets_host[n])
+        what = f"the first {n} payloads ({sample_bytes} B) of the offsets layout"
+    run(64)  # warm
     passes, t0 = 0, time.perf_counter()
     while True:
-        O.batch_fixed(method, host, length, length, n, variant=variant, nthreads=threads)
+        want = run(n)
         passes += 1
         el = time.perf_counter() - t0
         if el >= budget_s and passes >= 2:
             break
-    val = passes * n * length / el / 2**30
-    return {"value": round(val, 2), "unit": "GiB/s", "cores": threads, "kind": "port",
+    base = {"value": round(passes * sample_bytes / el / 2**30, 2), "unit": "GiB/s", "cores": threads, "kind": "port",
             "variant": "x86 SSE4.2 crc32 instruction" if variant == "sse42" else "slicing table",
-            "sample": f"{passes} passes over {n} x {length} B of the same splitmix payloads ({el:.2f} s wall)"}
+            "sample": f"{passes} passes over {what} of the same splitmix payloads ({el:.2f} s wall)"}
+
+    bad = int(np.count_nonzero(got[:n] != want))
+    rng = np.random.default_rng(1234)
+    total = len(got)
+    idx = np.unique(np.concatenate([[total - 1], rng.integers(n, total, samples)])) if total > n else []
+    for gi in idx:
+        gi = int(gi)
+        if offsets_host is None:
+            w = O.splitmix_batch_fixed(method, seed, length, length, gi, 1)[0]
+        else:
+            lo, hi = int(offsets_host[gi]), int(offsets_host[gi + 1])
+            w0 = lo // 8
+            b = O.splitmix_bytes(hi - w0 * 8, seed, first_word=w0)
+            w = O.crc(method, b[lo - w0 * 8:])
+        bad += int(got[gi] != w)
+    checked = n + len(idx)
+    parity = f"bit-exact ({checked} payloads vs oracle)" if bad == 0 else f"MISMATCH {bad}/{checked}"
+    return base, parity
+
+
+def cross_rank_check(G, method, seed, length, offsets_host, got, count, world, dev, samples):
+    """N>1 (rank 0): regenerate sampled payloads of EVERY shard on rank 0's GPU
+    and recompute them through the same entry point; the gathered CRCs must
+    agree (kernel parity itself is the N=1 oracle check and tests/)."""
+    if got is None:
+        return None
+    import torch
+    from mercury_amd.workload import varlen_offsets
+    rng = np.random.default_rng(4321)
+    bad = checked = 0
+    for r in range(world):
+        idx = np.unique(np.concatenate([[0, count - 1], rng.integers(0, count, max(1, samples // world))]))
+        off_r = None if offsets_host is None else varlen_offsets(seed ^ r, count)
+        for i in idx:
+            i = int(i)
+            if off_r is None:
+                buf = torch.empty(length + 64, dtype=torch.uint8, device=dev)
+                G.fill_splitmix(buf, seed, first_word=(r * count + i) * length // 8)
+                v = G.checksum_fixed(method, buf, length, count=1)
+            else:
+                lo, hi = int(off_r[i]), int(off_r[i + 1])
+                w0 = lo // 8
+                buf = torch.empty(hi - w0 * 8 + 64, dtype=torch.uint8, device=dev)
+                G.fill_splitmix(buf, seed ^ r, first_word=w0)
+                t = torch.tensor([lo - w0 * 8, hi - w0 * 8], dtype=torch.int64, device=dev)
+                v = G.checksum_offsets(method, buf, t)
+            bad += int(G.as_unsigned(v)[0] != got[r * count + i])
+            checked += 1
+    return (f"consistent ({checked} payloads across {world} shards recomputed on rank 0)" if bad == 0
+            else f"MISMATCH {bad}/{checked} across shards")
 
 
 if __name__ == "__main__":

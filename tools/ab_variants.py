@@ -68,8 +68,8 @@ def main():
         method, count, length, seed = SHAPES[cfg]
         offs = None
         if length is None:
-            from oracle import oracle as O
-            off_h = O.varlen_offsets(seed, count)
+            from mercury_amd.workload import varlen_offsets
+            off_h = varlen_offsets(seed, count)
             nbytes = int(off_h[-1])
             data = torch.empty(nbytes + 64, dtype=torch.uint8, device="cuda")
             offs = torch.from_numpy(off_h.astype(np.int64)).cuda()

@@ -12,14 +12,18 @@ for c in ${CONFIGS:-metric c2 c3 c4}; do
   timeout -k 10 300 python bench.py --config $c > $O/bench_$c.json 2> $O/bench_$c.err || { tail -20 $O/bench_$c.err; exit 1; }
   cat $O/bench_$c.json
 done
-step "torchrun 2 ranks (gloo rehearsal on one GPU)"
-timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --backend gloo --steps 5 --warmup 2 --no-cpu-baseline > $O/bench_2rank_gloo.json 2> $O/bench_2rank_gloo.err || { tail -20 $O/bench_2rank_gloo.err; exit 1; }
-cat $O/bench_2rank_gloo.json
+for c in metric c4; do
+  step "torchrun 2 ranks $c (gloo rehearsal on one GPU)"
+  timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --config $c --gpus 2 --backend gloo --steps 5 --warmup 2 > $O/bench_2rank_gloo_$c.json 2> $O/bench_2rank_gloo_$c.err || { tail -20 $O/bench_2rank_gloo_$c.err; exit 1; }
+  cat $O/bench_2rank_gloo_$c.json
+done
 cd /tmp && export TMPDIR=/tmp
 step "kernel trace"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_metric -o bench -- python3 $R/bench.py > $O/prof_bench.json 2> $O/prof_bench.err || { tail $O/prof_bench.err; exit 1; }
-step "pmc fetch"
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o pmc -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $O/pmc_fetch.json 2> $O/pmc_fetch.err || { tail $O/pmc_fetch.err; exit 1; }
-step "pmc write"
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o pmc -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $O/pmc_write.json 2> $O/pmc_write.err || { tail $O/pmc_write.err; exit 1; }
-python3 $R/tools/pmc_traffic.py $O/pmc_fetch $O/pmc_write crc32c_batch_kernel $O/pmc_traffic_metric.json 4295229440
+for c in ${PMC_CONFIGS:-metric c2 c3 c4}; do
+  k=crc32c_batch_kernel; [ $c = c3 ] && k=crc64_batch_kernel
+  step "pmc fetch/write $c"
+  timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch_$c -o pmc -- python3 $R/bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline > $O/pmc_fetch_$c.json 2> $O/pmc_fetch_$c.err || { tail $O/pmc_fetch_$c.err; exit 1; }
+  timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write_$c -o pmc -- python3 $R/bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline > $O/pmc_write_$c.json 2> $O/pmc_write_$c.err || { tail $O/pmc_write_$c.err; exit 1; }
+  python3 $R/tools/pmc_traffic.py $O/pmc_fetch_$c $O/pmc_write_$c $k $O/pmc_traffic_$c.json $(python3 $R/tools/alg_bytes.py $c)
+done

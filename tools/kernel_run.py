@@ -14,8 +14,8 @@ ap.add_argument("--iters", type=int, default=5)
 a = ap.parse_args()
 method, count, length, seed = SHAPES[a.config]
 if length is None:
-    from oracle import oracle as O
-    off = O.varlen_offsets(seed, count)
+    from mercury_amd.workload import varlen_offsets
+    off = varlen_offsets(seed, count)
     data = torch.empty(int(off[-1]) + 64, dtype=torch.uint8, device="cuda")
     G.fill_splitmix(data, seed)
     offs = torch.from_numpy(off.astype(np.int64)).cuda()
