@@ -16,7 +16,7 @@ EXTRA_HIPFLAGS ?=
 LIB       := $(LIBDIR)/libmchecksum.so
 BENCHLIB  := $(LIBDIR)/libmchecksum_bench.so
 COBJS     := $(BUILD)/mchecksum_cpu.o $(BUILD)/mchecksum_models.o $(BUILD)/crc_tables.o
-GOBJS     := $(BUILD)/mchecksum_gpu.o
+GOBJS     := $(BUILD)/mchecksum_gpu.o $(BUILD)/mchecksum_gpu_ext.o
 
 all: $(LIB) $(BENCHLIB) oracle $(BUILD)/c1_bench
 
@@ -27,6 +27,9 @@ $(BUILD)/%.o: $(CSRC)/%.c $(wildcard $(CSRC)/*.h) include/mchecksum.h | $(BUILD)
 	$(CC) $(CFLAGS) $(INC) -c $< -o $@
 
 $(BUILD)/mchecksum_gpu.o: $(CSRC)/mchecksum_gpu.hip $(wildcard $(CSRC)/*.h) include/mchecksum_gpu.h | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) $(EXTRA_HIPFLAGS) $(INC) -c $< -o $@
+
+$(BUILD)/mchecksum_gpu_ext.o: $(CSRC)/mchecksum_gpu_ext.hip $(wildcard $(CSRC)/*.h) include/mchecksum_gpu.h | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) $(EXTRA_HIPFLAGS) $(INC) -c $< -o $@
 
 $(BUILD)/bench_datagen.o: $(CSRC)/bench_datagen.hip | $(BUILD)
@@ -65,12 +68,12 @@ clean:
 # A/B variants of the batch kernels (tools/ab_variants.py).  Each is a full
 # libmchecksum built with different tuning macros.
 VARIANTS := base:-DMCK_RING=4 sdwa0:-DMCK_SDWA64=0 split1:-DMCK_CRC64_SPLIT=1 ring6:-DMCK_RING=6
-variants: $(COBJS) | $(BUILD)
+variants: $(COBJS) $(BUILD)/mchecksum_gpu_ext.o | $(BUILD)
 	mkdir -p $(BUILD)/variants
 	@for v in $(VARIANTS); do n=$${v%%:*}; f=$$(echo $${v#*:} | tr , " "); \
 	  echo "variant $$n: $$f"; \
 	  $(HIPCC) $(HIPFLAGS) $$f $(INC) -c $(CSRC)/mchecksum_gpu.hip -o $(BUILD)/variants/gpu_$$n.o && \
-	  $(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $(BUILD)/variants/libmchecksum_$$n.so $(COBJS) $(BUILD)/variants/gpu_$$n.o -lpthread || exit 1; \
+	  $(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $(BUILD)/variants/libmchecksum_$$n.so $(COBJS) $(BUILD)/variants/gpu_$$n.o $(BUILD)/mchecksum_gpu_ext.o -lpthread || exit 1; \
 	done
 .PHONY: variants
 

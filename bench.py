@@ -28,7 +28,8 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md:36
+HBM_PEAK_GBS = 8000.0
+SEGS_PER_OBJECT = 4  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md:36
 
 CONFIGS = {
     # name: (method, count, length, seed, layout)
@@ -36,6 +37,9 @@ CONFIGS = {
     "c2": ("crc32c", 65536, 4096, 0x4D43310000000002, "fixed"),
     "c3": ("crc64", 8192, 1 << 20, 0x4D43310000000003, "fixed"),
     "c4": ("crc32c", 262144, None, 0x4D43310000000004, "offsets"),
+    # 8(f) 2: C3's bytes as bulk-handle segment lists -- 8192 objects x 4
+    # segments of 256 KiB scattered over the buffer (permuted slots)
+    "seg": ("crc64", 8192, 1 << 20, 0x4D43310000000003, "segments"),
     # BASELINE configs[0]: host CPU, through the drop-in streaming API
     "c1": ("crc32c", 1024, 4096, 0x4D43310000000001, "cpu"),
 }
@@ -92,6 +96,17 @@ def main():
         offsets_dev = offsets_host = None
         payload_bytes = nbytes
         run = lambda out: G.checksum_fixed(method, data, length, count=count, out=out)  # noqa: E731
+    elif layout == "segments":
+        from mercury_amd.workload import segment_slots
+        seg_len = length // SEGS_PER_OBJECT
+        payload_bytes = count * length
+        data = torch.empty(payload_bytes + 64, dtype=torch.uint8, device=dev)
+        G.fill_splitmix(data, seed ^ rank)
+        slots = segment_slots(seed ^ rank, count * SEGS_PER_OBJECT)
+        batch = G.SegmentBatch([data[int(q) * seg_len:(int(q) + 1) * seg_len] for q in slots],
+                               np.arange(0, count * SEGS_PER_OBJECT + 1, SEGS_PER_OBJECT))
+        offsets_dev = offsets_host = None
+        run = lambda out: batch.checksum(method, out=out)  # noqa: E731
     else:
         from mercury_amd.workload import varlen_offsets
         offsets_host = varlen_offsets(seed ^ rank, count)
@@ -141,7 +156,8 @@ def main():
     total_bytes = payload_bytes * world * args.steps  # every rank checksummed its shard once per step
     gib_s = total_bytes / wall_max / 2**30
     out_bytes = count * (4 if G.out_dtype(method) == torch.int32 else 8)
-    alg_bytes = payload_bytes + out_bytes + (8 * (count + 1) if layout == "offsets" else 0)
+    alg_bytes = payload_bytes + out_bytes + (8 * (count + 1) if layout == "offsets" else 0) + \
+        (16 * count * SEGS_PER_OBJECT + 8 * (count + 1) if layout == "segments" else 0)
     achieved = alg_bytes / (kern_ms_max * 1e-3) / 1e9
 
     result = None
@@ -168,7 +184,8 @@ def main():
             "dtype": "u8",
             "data": "synthetic (splitmix64 bytes generated on device)",
             "config": {"workload": f"{method} over {count} x {length if length else 'U[64B,64KiB]'} B payloads per GPU"
-                       + (" (offsets table)" if layout == "offsets" else ""),
+                       + (" (offsets table)" if layout == "offsets" else "")
+                       + (f" ({SEGS_PER_OBJECT} scattered segments each)" if layout == "segments" else ""),
                        "method": method, "payloads_per_gpu": count, "payload_bytes": length,
                        "bytes_per_gpu": payload_bytes, "lanes_per_payload": G.lanes_per_payload(method, length or 65536)
                        if layout == "fixed" else 64, "parallelism": f"shard{world}"},
@@ -180,10 +197,11 @@ def main():
             # the only leg that runs the oracle: timed on a bounded sample, and
             # the checker of the GPU's values (that sample + random payloads)
             result["cpu_baseline"], result["parity"] = cpu_baseline(
-                method, seed, length, offsets_host, got, args.cpu_seconds, args.parity_samples)
+                method, seed, length, offsets_host, got, args.cpu_seconds, args.parity_samples,
+                segments=layout == "segments")
         elif world > 1:
             result["parity"] = cross_rank_check(G, method, seed, length, offsets_host, got, count, world, dev,
-                                                args.parity_samples)
+                                                args.parity_samples, segments=layout == "segments")
         else:
             result["parity"] = "unchecked (--no-cpu-baseline)"
         print(json.dumps(result), flush=True)
@@ -236,7 +254,14 @@ def bench_c1(args):
     return res
 
 
-def cpu_baseline(method, seed, length, offsets_host, got, budget_s, samples):
+def _segment_object_bytes(O, seed, length, j, slots):
+    """Host bytes of object j of the segments layout (oracle generator)."""
+    seg = length // SEGS_PER_OBJECT
+    return np.concatenate([O.splitmix_bytes(seg, seed, first_word=int(slots[j * SEGS_PER_OBJECT + q]) * seg // 8)
+                           for q in range(SEGS_PER_OBJECT)])
+
+
+def cpu_baseline(method, seed, length, offsets_host, got, budget_s, samples, segments=False):
     """The CPU leg (N=1, rank 0): the oracle (CPU restatement of mchecksum --
     the reference's own mchecksum is absent, so kind = "port") timed on this
     host's cores over a bounded sample of the same workload (the first n
@@ -245,7 +270,16 @@ def cpu_baseline(method, seed, length, offsets_host, got, budget_s, samples):
     from oracle import oracle as O
     threads = max(1, min(16, os.cpu_count() or 1))
     variant = "sse42" if method == "crc32c" else "table"
-    if offsets_host is None:
+    slots = None
+    if segments:
+        from mercury_amd.workload import segment_slots
+        slots = segment_slots(seed, len(got) * SEGS_PER_OBJECT)
+        n = 256
+        host = np.concatenate([_segment_object_bytes(O, seed, length, j, slots) for j in range(n)])
+        run = lambda k: O.batch_fixed(method, host, length, length, k, variant=variant, nthreads=threads)  # noqa: E731
+        sample_bytes = n * length
+        what = f"the first {n} objects ({SEGS_PER_OBJECT} x {length // SEGS_PER_OBJECT} B segments, gathered)"
+    elif offsets_host is None:
         n = 4096 if length <= 65536 else 256
         host = O.splitmix_bytes(n * length, seed)
         run = lambda k: O.batch_fixed(method, host, length, length, k, variant=variant, nthreads=threads)  # noqa: E731
@@ -276,7 +310,9 @@ def cpu_baseline(method, seed, length, offsets_host, got, budget_s, samples):
     idx = np.unique(np.concatenate([[total - 1], rng.integers(n, total, samples)])) if total > n else []
     for gi in idx:
         gi = int(gi)
-        if offsets_host is None:
+        if segments:
+            w = O.crc(method, _segment_object_bytes(O, seed, length, gi, slots))
+        elif offsets_host is None:
             w = O.splitmix_batch_fixed(method, seed, length, length, gi, 1)[0]
         else:
             lo, hi = int(offsets_host[gi]), int(offsets_host[gi + 1])
@@ -289,7 +325,7 @@ def cpu_baseline(method, seed, length, offsets_host, got, budget_s, samples):
     return base, parity
 
 
-def cross_rank_check(G, method, seed, length, offsets_host, got, count, world, dev, samples):
+def cross_rank_check(G, method, seed, length, offsets_host, got, count, world, dev, samples, segments=False):
     """N>1 (rank 0): regenerate sampled payloads of EVERY shard on rank 0's GPU
     and recompute them through the same entry point; the gathered CRCs must
     agree (kernel parity itself is the N=1 oracle check and tests/)."""
@@ -302,9 +338,20 @@ def cross_rank_check(G, method, seed, length, offsets_host, got, count, world, d
     for r in range(world):
         idx = np.unique(np.concatenate([[0, count - 1], rng.integers(0, count, max(1, samples // world))]))
         off_r = None if offsets_host is None else varlen_offsets(seed ^ r, count)
+        if segments:
+            from mercury_amd.workload import segment_slots
+            slots = segment_slots(seed ^ r, count * SEGS_PER_OBJECT)
         for i in idx:
             i = int(i)
-            if off_r is None:
+            if segments:
+                seg = length // SEGS_PER_OBJECT
+                parts = []
+                for q in range(SEGS_PER_OBJECT):
+                    t = torch.empty(seg + 64, dtype=torch.uint8, device=dev)
+                    G.fill_splitmix(t, seed ^ r, first_word=int(slots[i * SEGS_PER_OBJECT + q]) * seg // 8)
+                    parts.append(t[:seg])
+                v = G.checksum_segments(method, parts)
+            elif off_r is None:
                 buf = torch.empty(length + 64, dtype=torch.uint8, device=dev)
                 G.fill_splitmix(buf, seed, first_word=(r * count + i) * length // 8)
                 v = G.checksum_fixed(method, buf, length, count=1)

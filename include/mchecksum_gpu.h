@@ -96,6 +96,48 @@ mchecksum_gpu_verify_messages(const char *hash_method, const void *dev_buf,
     size_t hash_offset, uint8_t *dev_status, uint32_t *dev_mismatches,
     void *stream);
 
+/* Scatter-gather objects: object j is the
+ * concatenation, in order, of segments [dev_obj_first[j], dev_obj_first[j+1])
+ * of the segment list (dev_seg_addr[s], dev_seg_len[s]) -- the shape of a bulk
+ * handle's segments, HG_Bulk_create(count, buf_ptrs, buf_sizes)
+ * (src/mercury_bulk.h:55,79), registered as device memory (hg_bulk_attr
+ * mem_type HG_MEM_TYPE_ROCM, src/mercury_types.h:38,44-47).  dev_out[j] =
+ * mchecksum_get() after one mchecksum_update() per segment of object j
+ * (count = nobj host-order values; an object with no bytes gets the CRC of the
+ * empty message).  All arrays are device-resident: dev_seg_addr holds device
+ * addresses (each segment readable to its next 16-byte boundary),
+ * dev_obj_first holds nobj + 1 non-decreasing indices <= nseg; segments
+ * outside [first[0], first[nobj]) are ignored.  dev_work: caller-owned device
+ * scratch (8-byte aligned) of at least mchecksum_gpu_segments_work_size(nseg)
+ * bytes, not shared with a concurrent call.  crc32c and crc64.  Segments are
+ * cut into 256 KiB chunks hashed in parallel and recombined with GF(2) shift
+ * operators, so one huge segment still spreads over the whole GPU. */
+MCHECKSUM_PUBLIC size_t
+mchecksum_gpu_segments_work_size(size_t nseg);
+
+MCHECKSUM_PUBLIC int
+mchecksum_gpu_checksum_segments(const char *hash_method,
+    const uint64_t *dev_seg_addr, const uint64_t *dev_seg_len, size_t nseg,
+    const uint64_t *dev_obj_first, size_t nobj, void *dev_work,
+    size_t work_size, void *dev_out, void *stream);
+
+/* Batched check of Mercury core headers for received
+ * messages in device memory: message i = dev_buf[dev_msg_offsets[i],
+ * dev_msg_offsets[i+1]) starts with the 16-byte core header that
+ * hg_core_header_request_proc / _response_proc encode
+ * (src/mercury_core_header.c:175-289).  The 16-bit hash_method ("crc16") is
+ * recomputed over the host-order field values exactly as those functions
+ * stream them into mchecksum_update and compared with the big-endian hash on
+ * the wire (request: offset 12, response: offset 4).  dev_status[i] = 1 on a
+ * mismatch or a message shorter than 16 bytes (HG_CHECKSUM_ERROR /
+ * HG_INVALID_ARG in Mercury); *dev_mismatches is incremented per failure. */
+#define MCHECKSUM_GPU_CORE_HEADER_REQUEST  0
+#define MCHECKSUM_GPU_CORE_HEADER_RESPONSE 1
+MCHECKSUM_PUBLIC int
+mchecksum_gpu_verify_core_headers(const char *hash_method, int kind,
+    const void *dev_buf, const uint64_t *dev_msg_offsets, size_t count,
+    uint8_t *dev_status, uint32_t *dev_mismatches, void *stream);
+
 /* Lanes cooperating on one payload that checksum_fixed would choose for
  * this length (1..64), for reporting; -1 on error. */
 MCHECKSUM_PUBLIC int

@@ -21,7 +21,9 @@ STREAMING_SYMBOLS = ("mchecksum_init", "mchecksum_destroy", "mchecksum_reset", "
                      "mchecksum_get", "mchecksum_update")
 GPU_SYMBOLS = ("mchecksum_gpu_available", "mchecksum_gpu_prepare", "mchecksum_gpu_checksum_fixed",
                "mchecksum_gpu_checksum_offsets", "mchecksum_gpu_verify_offsets", "mchecksum_gpu_verify_messages",
-               "mchecksum_gpu_lanes_per_payload", "mchecksum_gpu_last_error")
+               "mchecksum_gpu_lanes_per_payload", "mchecksum_gpu_last_error", "mchecksum_gpu_segments_work_size",
+               "mchecksum_gpu_checksum_segments", "mchecksum_gpu_verify_core_headers")
+CORE_HEADER_REQUEST, CORE_HEADER_RESPONSE = 0, 1
 
 _lib = None
 _bench = None
@@ -65,6 +67,14 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     L.mchecksum_gpu_verify_messages.restype = c_int
     L.mchecksum_gpu_lanes_per_payload.argtypes = [c_char_p, c_size_t]
     L.mchecksum_gpu_lanes_per_payload.restype = c_int
+    L.mchecksum_gpu_segments_work_size.argtypes = [c_size_t]
+    L.mchecksum_gpu_segments_work_size.restype = c_size_t
+    L.mchecksum_gpu_checksum_segments.argtypes = [c_char_p, c_void_p, c_void_p, c_size_t, c_void_p, c_size_t,
+                                                  c_void_p, c_size_t, c_void_p, c_void_p]
+    L.mchecksum_gpu_checksum_segments.restype = c_int
+    L.mchecksum_gpu_verify_core_headers.argtypes = [c_char_p, c_int, c_void_p, c_void_p, c_size_t, c_void_p,
+                                                    c_void_p, c_void_p]
+    L.mchecksum_gpu_verify_core_headers.restype = c_int
     L.mchecksum_gpu_last_error.argtypes = []
     L.mchecksum_gpu_last_error.restype = c_char_p
     _lib = L

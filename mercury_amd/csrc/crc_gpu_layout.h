@@ -48,6 +48,17 @@ typedef struct {
     uint32_t nops;
 } crc64_gpu_pack_t;
 
+/* ---- register shifts Z^n for 0 <= n < 2^48 (scatter-gather combine) ----- */
+/* Z^n = prod over base-16 digits d_k of n of Z^(d_k * 16^k): at most 12
+ * operator applications.  op[k][d-1] = nibble tables of Z^(d * 16^k).       */
+#define CRC_SHIFT_DIGITS 12
+typedef struct {
+    uint32_t op[CRC_SHIFT_DIGITS][15][8][16];
+} crc32_shift_pack_t;
+typedef struct {
+    uint64_t op[CRC_SHIFT_DIGITS][15][16][16];
+} crc64_shift_pack_t;
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -63,6 +74,8 @@ typedef struct {
 /* Host generators (crc_tables.c). Return 0 on success. */
 int crc32_gpu_pack_build(const crc_rmodel_t *m, int log2g, crc32_gpu_pack_t *out);
 int crc64_gpu_pack_build(const crc_rmodel_t *m, int log2g, crc64_gpu_pack_t *out);
+int crc32_shift_pack_build(const crc_rmodel_t *m, crc32_shift_pack_t *out);
+int crc64_shift_pack_build(const crc_rmodel_t *m, crc64_shift_pack_t *out);
 
 /* GF(2) operator helpers (W x W bit matrices stored as W column words). */
 void crc_op_zero_byte(const crc_rmodel_t *m, uint64_t *col);

@@ -252,3 +252,60 @@ crc64_gpu_pack_build(const crc_rmodel_t *m, int log2g, crc64_gpu_pack_t *out)
     out->nops = (uint32_t) o;
     return 0;
 }
+
+/* Z^(d * 16^k) for d = 1..15, k < CRC_SHIFT_DIGITS, by repeated products of
+ * Z^(16^k) (no per-entry matrix powers). */
+static int
+shift_ops(const crc_rmodel_t *m, void (*emit)(void *, int, int, const uint64_t *), void *out)
+{
+    uint64_t base[64], cur[64], nxt[64];
+    int k, d, w = m->width;
+
+    crc_op_zero_byte(m, base); /* Z^(16^0) */
+    for (k = 0; k < CRC_SHIFT_DIGITS; k++) {
+        memcpy(cur, base, sizeof(cur));
+        for (d = 1; d <= 15; d++) {
+            emit(out, k, d, cur);
+            crc_op_mul(w, cur, base, nxt);
+            memcpy(cur, nxt, sizeof(cur));
+        }
+        memcpy(base, cur, sizeof(base)); /* Z^(16^(k+1)) = Z^(16 * 16^k) */
+    }
+    return 0;
+}
+
+static void
+emit32(void *o, int k, int d, const uint64_t *op)
+{
+    crc32_shift_pack_t *out = (crc32_shift_pack_t *) o;
+    int h, v;
+    for (h = 0; h < 8; h++)
+        for (v = 0; v < 16; v++)
+            out->op[k][d - 1][h][v] = (uint32_t) crc_op_apply(32, op, (uint64_t) v << (4 * h));
+}
+
+static void
+emit64(void *o, int k, int d, const uint64_t *op)
+{
+    crc64_shift_pack_t *out = (crc64_shift_pack_t *) o;
+    int h, v;
+    for (h = 0; h < 16; h++)
+        for (v = 0; v < 16; v++)
+            out->op[k][d - 1][h][v] = crc_op_apply(64, op, (uint64_t) v << (4 * h));
+}
+
+int
+crc32_shift_pack_build(const crc_rmodel_t *m, crc32_shift_pack_t *out)
+{
+    if (!m || !out || m->width != 32)
+        return -1;
+    return shift_ops(m, emit32, out);
+}
+
+int
+crc64_shift_pack_build(const crc_rmodel_t *m, crc64_shift_pack_t *out)
+{
+    if (!m || !out || m->width != 64)
+        return -1;
+    return shift_ops(m, emit64, out);
+}

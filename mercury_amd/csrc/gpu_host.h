@@ -1,0 +1,40 @@
+// gpu_host.h -- host-side plumbing shared by the batch-kernel translation
+// units (mchecksum_gpu.hip, mchecksum_gpu_ext.hip): per-device table packs,
+// error text, launch helpers.  Internal (hidden visibility), not part of the ABI.
+#ifndef MCK_GPU_HOST_H
+#define MCK_GPU_HOST_H
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <mutex>
+
+#include "crc_gpu_device.h"
+#include "mchecksum_models.h"
+
+namespace mck {
+
+constexpr int kMaxDev = 64;
+
+struct DevCtx {
+    bool init = false;
+    int cus = 0;
+    void *pack[MCK_NMODELS][CRC_GPU_MAX_LOG2G + 1] = {};
+    void *ext[MCK_NMODELS] = {};  // mchecksum_gpu_ext.hip's per-model tables
+};
+
+extern std::mutex g_mu;
+
+// Record a formatted error for mchecksum_gpu_last_error(); returns rc.
+int set_err(int rc, const char *fmt, const char *a = "", int b = 0);
+int hip_err(hipError_t e, const char *what);
+// Method -> model index for GPU batch kernels (reflected 32/64-bit): -1 unknown, -2 no kernel.
+int gpu_model(const char *method, int *width);
+// Current device's context (caller holds g_mu).
+int device_ctx(DevCtx **out);
+// Model + device context + table pack for lanes-per-payload 2^log2g (takes g_mu).
+int prologue(const char *method, int log2g, int *width, DevCtx **c, const void **pack);
+
+}  // namespace mck
+
+#endif  // MCK_GPU_HOST_H

@@ -31,814 +31,17 @@
 #include <cstring>
 #include <mutex>
 
-#include "crc_gpu_layout.h"
-#include "crc_gpu_mask.h"
+#include "crc_gpu_device.h"
+#include "gpu_host.h"
 #include "mchecksum_gpu.h"
 #include "mchecksum_models.h"
 
-namespace {
-
-// Build-time tuning knobs (A/B builds: tools/ab_variants.py); defaults are
-// the measured best.
-#ifndef MCK_BLOCK
-#define MCK_BLOCK 1024
-#endif
-#ifndef MCK_RING
-#define MCK_RING 4
-#endif
-#ifndef MCK_BITOP3
-#define MCK_BITOP3 1
-#endif
-constexpr int kBlock = MCK_BLOCK;  // 1024 = 16 waves: 4 per SIMD
-constexpr int kRing = MCK_RING;  // dwordx4 pieces in flight per lane
-// Offsets batches (one payload per wave, ~32 KiB average) want a deeper ring:
-// 8 measured +4% over 4 on C4, while 8 costs 1-5% on the aligned batches.
-#ifndef MCK_RING_OFFSETS
-#define MCK_RING_OFFSETS 8
-#endif
-constexpr int kRingOff = MCK_RING_OFFSETS;
-
-// CRC-32C LDS map: [0,128K) main byte tables x32 copies; then op nibble tables.
-constexpr uint32_t kL32Main = 131072;
-constexpr uint32_t kL32Bytes = kL32Main + CRC32_NOPS_MAX * 512;
-// Light layout for small batches: the 4 byte tables unreplicated (4 KiB, so
-// the per-workgroup LDS fill is 16 KiB instead of 140 KiB) and 256-thread
-// workgroups spread over every CU; lookups may bank-conflict, which a small
-// batch never notices.
-constexpr uint32_t kL32LightMain = 4096;
-constexpr uint32_t kL32LightBytes = kL32LightMain + CRC32_NOPS_MAX * 512;
-constexpr int kLightBlock = 256;
-
-// CRC-32C table access policy: Tab32<false> = 32x-replicated conflict-free
-// layout (throughput), Tab32<true> = light layout (latency of small batches).
-template <bool LIGHT>
-struct Tab32 {
-    const uint8_t *lds;
-};
-// CRC-64 LDS map.  A 64-bit state is looked up by nibble: the 8 low-nibble
-// tables are replicated 32x (entry v at v*256 B, lane copy at (lane%32)*8 B;
-// the address is one v_perm of the masked nibble and the lane byte), the 8
-// high-nibble tables are NOT replicated: entry v sits at v*16 B, so the masked
-// byte (v << 4) is its own address and the 16 entries fall on 16 distinct bank
-// pairs of ds_read_b64 (lanes that share an entry broadcast) -- conflict-free
-// without copies.  Then the combine operators (nibble tables, 2 KiB each).
-constexpr uint32_t kL64Hi = 32768;
-constexpr uint32_t kL64Main = kL64Hi + 8 * 256;
-constexpr uint32_t kL64Bytes = kL64Main + CRC64_NOPS_MAX * 2048;
-// CRC-64 is VALU-bound (the table XOR tree); two 1024-thread workgroups per CU
-// (8 waves/SIMD, 80 KiB LDS each) hide the LDS latency.  MCK_CRC64_SPLIT=1
-// reads the combine operators (touched once per payload) from global memory
-// instead of LDS on the aligned path.
-#ifndef MCK_CRC64_SPLIT
-#define MCK_CRC64_SPLIT 0
-#endif
-#ifndef MCK_BLOCK64
-#define MCK_BLOCK64 1024
-#endif
-// Fold the next data word into the table-XOR tree (its 17th input slot is
-// free) and run the aligned step loop without per-step bounds tests.
-#ifndef MCK_LA64
-#define MCK_LA64 1
-#endif
-
-template <int W, int MODE, bool LIGHT = false>
-struct Shape {
-    static constexpr bool ops_global = W == 64 && MODE == 0 && MCK_CRC64_SPLIT;  // 0 = kFixedAligned
-    static constexpr bool two = W == 64 && MODE == 0;
-    static constexpr int block = LIGHT ? kLightBlock : two ? MCK_BLOCK64 : kBlock;
-    static constexpr int blocks_per_cu = LIGHT ? 8 : two ? 2 : 1;
-    static constexpr uint32_t lds64_bytes = ops_global ? kL64Main : kL64Bytes;
-};
-// single-argument aliases (a comma inside __launch_bounds__ splits the macro)
-template <int MODE>
-constexpr int kBlk64 = Shape<64, MODE>::block;
-template <int MODE>
-constexpr int kWpe64 = Shape<64, MODE>::blocks_per_cu * Shape<64, MODE>::block / 256;
-
-enum Mode : int { kFixedAligned = 0, kFixedGeneric = 1, kOffsets = 2 };
-
-struct BatchArgs {
-    const uint8_t *base;
-    const uint64_t *offsets;
-    uint64_t stride, len, count;
-    void *out;
-    const void *expected;
-    uint8_t *status;
-    uint32_t *mismatches;
-    const void *pack;
-    // message mode (verify_messages): payload i = [offsets[i] + pay_off,
-    // offsets[i+1]), expected CRC = big-endian u32 at offsets[i] + hash_off
-    uint32_t msg, pay_off, hash_off;
-};
-
-// Network-order u32 at an arbitrary byte address (the HG header's payload
-// hash, src/mercury_header.c:111-112 writes it with htonl).
-__device__ __forceinline__ uint32_t load_be32(const uint8_t *q) {
-    return (uint32_t)q[0] << 24 | (uint32_t)q[1] << 16 | (uint32_t)q[2] << 8 | (uint32_t)q[3];
-}
-
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-
-// Payload bytes are read exactly once.  Non-temporal loads keep a batch far
-// larger than the 256 MiB Infinity Cache from churning the caches: +13% on the
-// 4 GiB headline batch (profiles/r01/ab1.log); a small batch replayed
-// back to back is faster with the default policy (it partly hits the cache).
-template <bool NT>
-__device__ __forceinline__ uint4 ld16(const uint4 *p) {
-    if constexpr (NT) {
-        const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t *>(p));
-        return make_uint4(v.x, v.y, v.z, v.w);
-    } else {
-        return *p;
-    }
-}
-
-__device__ __forceinline__ uint32_t lds32(const uint8_t *lds, uint32_t a) {
-    return *reinterpret_cast<const uint32_t *>(lds + a);
-}
-__device__ __forceinline__ uint64_t lds64(const uint8_t *lds, uint32_t a) {
-    return *reinterpret_cast<const uint64_t *>(lds + a);
-}
-
-// ---------------------------------------------------------------- CRC-32C --
-
-// a ^ b ^ c in one VALU op: gfx950's v_bitop3_b32 with truth table 0x96
-// (there is no v_xor3_b32 on CDNA; hipcc does not form bitop3 from ^ chains).
-__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
-#if MCK_BITOP3
-    uint32_t r;
-    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-    return r;
-#else
-    return a ^ b ^ c;
-#endif
-}
-
-// Z^(16G)(x): main[p][byte_p(x)], tables p=0,1 in LDS region 0 (lc0), p=2,3
-// in region 1 (lc1 has +64 KiB in its byte 2); odd p at +128 B.  One step of
-// a sub-stream costs 4 v_perm + 2 v_bitop3 (+1 XOR with the data word) per
-// 4 bytes.  (Folding the next word into this XOR tree instead -- a look-ahead
-// pipeline -- measured 7% slower on the headline batch, profiles/r01/ab3.log.)
-__device__ __forceinline__ uint32_t f32s(Tab32<false> t, uint32_t x, uint32_t lc0, uint32_t lc1) {
-    const uint32_t a0 = __builtin_amdgcn_perm(x, lc0, 0x0C020400u);
-    const uint32_t a1 = __builtin_amdgcn_perm(x, lc0, 0x0C020500u);
-    const uint32_t a2 = __builtin_amdgcn_perm(x, lc1, 0x0C020600u);
-    const uint32_t a3 = __builtin_amdgcn_perm(x, lc1, 0x0C020700u);
-    return xor3(lds32(t.lds, a0), lds32(t.lds, a1 + 128), lds32(t.lds, a2)) ^ lds32(t.lds, a3 + 128);
-}
-
-__device__ __forceinline__ uint32_t f32s(Tab32<true> t, uint32_t x, uint32_t, uint32_t) {
-    const uint32_t a0 = (x << 2) & 0x3FCu, a1 = (x >> 6) & 0x3FCu, a2 = (x >> 14) & 0x3FCu, a3 = (x >> 22) & 0x3FCu;
-    return xor3(lds32(t.lds, a0), lds32(t.lds, a1 + 1024), lds32(t.lds, a2 + 2048)) ^ lds32(t.lds, a3 + 3072);
-}
-
-template <bool LIGHT>
-__device__ __forceinline__ uint32_t op32(Tab32<LIGHT> tab, uint32_t o, uint32_t x) {
-    const uint32_t base = (LIGHT ? kL32LightMain : kL32Main) + o * 512;
-    uint32_t t[8];
-#pragma unroll
-    for (int h = 0; h < 8; h++) t[h] = lds32(tab.lds, base + h * 64 + (((x >> (4 * h)) & 15u) << 2));
-    return xor3(xor3(t[0], t[1], t[2]), xor3(t[3], t[4], t[5]), t[6] ^ t[7]);
-}
-
-template <int LOG2G, class TAB>
-__device__ __forceinline__ uint32_t combine32(TAB lds, uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3,
-                                              uint32_t gl) {
-    uint32_t x = s0 ^ op32(lds, 0, s1);
-    const uint32_t y = s2 ^ op32(lds, 0, s3);
-    x ^= op32(lds, 1, y);
-#pragma unroll
-    for (int k = 0; k < LOG2G; k++) {
-        const uint32_t other = __shfl_xor(x, 1 << k, 64);
-        const bool bit = (gl >> k) & 1u;
-        const uint32_t lo = bit ? other : x, hi = bit ? x : other;
-        x = lo ^ op32(lds, 2 + k, hi);
-    }
-    return x;
-}
-
-template <bool LIGHT, int BLOCK>
-__device__ void fill_lds32(uint8_t *lds, const crc32_gpu_pack_t *pk) {
-    uint32_t *l = reinterpret_cast<uint32_t *>(lds);
-    if constexpr (LIGHT) {
-        const uint32_t *m = &pk->main[0][0];
-        for (uint32_t d = threadIdx.x; d < 1024u; d += BLOCK) l[d] = m[d];
-    } else {
-        for (uint32_t d = threadIdx.x; d < 32768u; d += BLOCK) {
-            const uint32_t region = d >> 14, e = (d >> 6) & 255u, half = (d >> 5) & 1u;
-            l[d] = pk->main[2 * region + half][e];
-        }
-    }
-    const uint32_t *ops = &pk->ops[0][0][0];
-    const uint32_t nops = pk->nops * 128u;
-    const uint32_t base = (LIGHT ? kL32LightMain : kL32Main) / 4;
-    for (uint32_t d = threadIdx.x; d < nops; d += BLOCK) l[base + d] = ops[d];
-}
-
-// Ring slot j % kRing holds the piece of step j, loaded kRing steps ahead.
-//
-// Aligned fixed-size payload: base 16-B aligned, len = K * 16G, no masking,
-// no pad bytes (tail op is the identity and is skipped).
-template <int LOG2G, bool NT, class TAB>
-__device__ __forceinline__ uint32_t payload32_aligned(TAB lds, const uint8_t *p, uint64_t K, uint32_t gl,
-                                                      uint32_t lc0, uint32_t lc1, uint32_t init) {
-    constexpr int G = 1 << LOG2G;
-    const uint4 *src = reinterpret_cast<const uint4 *>(p) + gl;
-    uint4 ring[kRing];
-#pragma unroll
-    for (int u = 0; u < kRing; u++) ring[u] = (uint64_t)u < K ? ld16<NT>(src + (uint64_t)u * G) : make_uint4(0, 0, 0, 0);
-    uint32_t x0 = gl == 0 ? init : 0u, x1 = 0, x2 = 0, x3 = 0;
-    for (uint64_t k = 0; k < K; k += kRing) {
-#pragma unroll
-        for (int u = 0; u < kRing; u++) {
-            const uint4 v = ring[u];
-            const uint64_t kn = k + u + kRing;
-            if (kn < K) ring[u] = ld16<NT>(src + kn * G);
-            if (k + u < K) {
-                x0 = f32s(lds, x0 ^ v.x, lc0, lc1);
-                x1 = f32s(lds, x1 ^ v.y, lc0, lc1);
-                x2 = f32s(lds, x2 ^ v.z, lc0, lc1);
-                x3 = f32s(lds, x3 ^ v.w, lc0, lc1);
-            }
-        }
-    }
-    return combine32<LOG2G>(lds, x0, x1, x2, x3, gl);
-}
-
-template <typename T>
-__device__ __forceinline__ T wave_max(T v) {
-#pragma unroll
-    for (int k = 1; k < 64; k <<= 1) {
-        const T o = __shfl_xor(v, k, 64);
-        v = o > v ? o : v;
-    }
-    return v;
-}
-
-// Any alignment, any length (0 included).  Per-lane window; the wave loops to
-// the largest step count of its groups.
-template <int LOG2G, bool NT, class TAB>
-__device__ __forceinline__ uint32_t payload32_generic(TAB lds, const crc32_gpu_pack_t *pk,
-                                                      const uint8_t *p, uint64_t len, uint32_t gl, uint32_t lc0,
-                                                      uint32_t lc1) {
-    constexpr int G = 1 << LOG2G;
-    constexpr int64_t step = 16 * G;
-    const uint32_t init = pk->init;
-    const uint64_t sa = reinterpret_cast<uint64_t>(p), ea = sa + len;
-    const uint64_t a0 = sa & ~15ull, a1 = (ea + 15) & ~15ull;
-    const int64_t W = (int64_t)(a1 - a0);
-    const int64_t K = (W + step - 1) >> (4 + LOG2G);
-    const int64_t r0 = W - K * step;
-    const int64_t hs = (int64_t)(sa - a0), he = (int64_t)(ea - a0);
-    const int64_t ilen = (int64_t)len;
-    const int64_t kmax = LOG2G == 6 ? K : wave_max(K);
-    const int64_t lane_off = 16 * (int64_t)gl;
-
-    auto fetch = [&](int64_t k) -> uint4 {
-        const int64_t pc = r0 + k * step + lane_off;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (k < K && pc >= 0) v = ld16<NT>(reinterpret_cast<const uint4 *>(a0 + (uint64_t)pc));
-        return v;
-    };
-    // edge handling (crc_gpu_mask.h) for the piece of step k < K
-    auto prep = [&](int64_t k, uint4 v) -> uint4 {
-        const int64_t pc = r0 + k * step + lane_off;
-        if (!mck_piece_clean(pc, hs, he, 4)) {
-            const int64_t lo = pc - hs;
-            v.x = mck_mask32(v.x, lo, ilen, init);
-            v.y = mck_mask32(v.y, lo + 4, ilen, init);
-            v.z = mck_mask32(v.z, lo + 8, ilen, init);
-            v.w = mck_mask32(v.w, lo + 12, ilen, init);
-        }
-        return v;
-    };
-
-    uint4 ring[kRing];
-#pragma unroll
-    for (int u = 0; u < kRing; u++) ring[u] = fetch(u);
-    uint32_t x0 = 0, x1 = 0, x2 = 0, x3 = 0;
-    for (int64_t k = 0; k < kmax; k += kRing) {
-#pragma unroll
-        for (int u = 0; u < kRing; u++) {
-            const int64_t j = k + u;
-            const uint4 raw = ring[u];
-            ring[u] = fetch(j + kRing);
-            if (j < K) {
-                const uint4 w = prep(j, raw);
-                x0 = f32s(lds, x0 ^ w.x, lc0, lc1);
-                x1 = f32s(lds, x1 ^ w.y, lc0, lc1);
-                x2 = f32s(lds, x2 ^ w.z, lc0, lc1);
-                x3 = f32s(lds, x3 ^ w.w, lc0, lc1);
-            }
-        }
-    }
-    uint32_t x = combine32<LOG2G>(lds, x0, x1, x2, x3, gl);
-    x = op32(lds, 2 + LOG2G + (uint32_t)(a1 - ea), x);
-    if (len < 4) x ^= pk->zinit[len];
-    return x;
-}
-
-// One payload per wave (G = 64): the window geometry is wave-uniform, so the
-// payload base stays in SGPRs, each lane carries a 32-bit offset (saddr-form
-// global loads), and "does this step touch an edge?" is a scalar test -- only
-// the first/last steps pay for per-lane masking.  Payloads < 2 GiB.
-template <bool NT, class TAB>
-__device__ __forceinline__ uint32_t payload32_g64(TAB lds, const crc32_gpu_pack_t *pk, const uint8_t *p,
-                                                  uint64_t len, uint32_t gl, uint32_t lc0, uint32_t lc1) {
-    const uint32_t init = pk->init;
-    const uint64_t sa = reinterpret_cast<uint64_t>(p), ea = sa + len;
-    const uint64_t a0 = sa & ~15ull, a1 = (ea + 15) & ~15ull;
-    const uint32_t W = (uint32_t)(a1 - a0);
-    const uint32_t K = (W + 1023u) >> 10;
-    const uint32_t lead = K * 1024u - W;                 // window starts `lead` bytes into step 0
-    const uint8_t *wb = reinterpret_cast<const uint8_t *>(a0 - lead);  // step grid origin (uniform)
-    const uint32_t qs = lead + (uint32_t)(sa - a0);      // payload [qs, qe) relative to wb
-    const uint32_t qe = lead + (uint32_t)(ea - a0);
-    const int32_t ilen = (int32_t)len;
-    const uint32_t lo_lane = 16u * gl;
-    // steps [kc0, kc1) are clean for every lane
-    const uint32_t kc0 = (qs + 4u + 1023u) >> 10;
-    const uint32_t kc1 = qe >= 1024u ? (qe - 1024u) / 1024u + 1u : 0u;
-
-    auto fetch = [&](uint32_t k) -> uint4 {
-        const uint32_t q = k * 1024u + lo_lane;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (k < K && q >= lead) v = ld16<NT>(reinterpret_cast<const uint4 *>(wb + q));
-        return v;
-    };
-
-    uint32_t x0 = 0, x1 = 0, x2 = 0, x3 = 0;
-    uint4 ring[kRingOff];
-#pragma unroll
-    for (int u = 0; u < kRingOff; u++) ring[u] = fetch(u);
-    for (uint32_t k = 0; k < K; k += kRingOff) {
-#pragma unroll
-        for (int u = 0; u < kRingOff; u++) {
-            uint4 v = ring[u];
-            const uint32_t kk = k + u;
-            ring[u] = fetch(kk + kRingOff);
-            if (kk < K) {
-                if (kk < kc0 || kk >= kc1) {  // wave-uniform: an edge step
-                    const int32_t lo = (int32_t)(kk * 1024u + lo_lane) - (int32_t)qs;
-                    v.x = mck_mask32(v.x, lo, ilen, init);
-                    v.y = mck_mask32(v.y, lo + 4, ilen, init);
-                    v.z = mck_mask32(v.z, lo + 8, ilen, init);
-                    v.w = mck_mask32(v.w, lo + 12, ilen, init);
-                }
-                x0 = f32s(lds, x0 ^ v.x, lc0, lc1);
-                x1 = f32s(lds, x1 ^ v.y, lc0, lc1);
-                x2 = f32s(lds, x2 ^ v.z, lc0, lc1);
-                x3 = f32s(lds, x3 ^ v.w, lc0, lc1);
-            }
-        }
-    }
-    uint32_t x = combine32<6>(lds, x0, x1, x2, x3, gl);
-    x = op32(lds, 2 + 6 + (uint32_t)(a1 - ea), x);
-    if (len < 4) x ^= pk->zinit[len];
-    return x;
-}
-
-// Byte-balanced static partition of an offsets batch: wave w owns payloads
-// whose start offset lies in [off0 + total*w/nw, off0 + total*(w+1)/nw).
-__device__ __forceinline__ uint64_t lower_bound_u64(const uint64_t *a, uint64_t n, uint64_t key) {
-    uint64_t lo = 0, hi = n;
-    while (lo < hi) {
-        const uint64_t mid = lo + ((hi - lo) >> 1);
-        if (a[mid] < key) lo = mid + 1;
-        else hi = mid;
-    }
-    return lo;
-}
-
-__device__ __forceinline__ void wave_range(const uint64_t *off, uint64_t count, uint32_t wave, uint32_t nw,
-                                           uint64_t *first, uint64_t *last) {
-    const uint64_t o0 = off[0], total = off[count] - o0;
-    const uint64_t q = total / nw, r = total % nw;
-    const uint64_t lo = o0 + q * wave + (r * wave) / nw;
-    const uint64_t hi = o0 + q * (wave + 1) + (r * (wave + 1)) / nw;
-    *first = wave == 0 ? 0 : lower_bound_u64(off, count, lo);
-    *last = wave + 1 == nw ? count : lower_bound_u64(off, count, hi);
-}
-
-template <typename T, bool VERIFY>
-__device__ __forceinline__ void emit(const BatchArgs &a, uint64_t p, T v) {
-    if (VERIFY) {
-        const bool bad = reinterpret_cast<const T *>(a.expected)[p] != v;
-        if (a.status) a.status[p] = bad ? 1 : 0;
-        if (bad && a.mismatches) atomicAdd(a.mismatches, 1u);
-    } else {
-        reinterpret_cast<T *>(a.out)[p] = v;
-    }
-}
-
-template <bool LIGHT>
-constexpr int kBlk32 = LIGHT ? kLightBlock : kBlock;
-
-template <int LOG2G, int MODE, bool VERIFY, bool NT, bool LIGHT = false>
-__global__ __launch_bounds__(kBlk32<LIGHT>, 1) void crc32c_batch_kernel(BatchArgs a) {
-    constexpr int kWavesPerBlock = kBlk32<LIGHT> / 64;
-    __shared__ __attribute__((aligned(16))) uint8_t lds_raw[LIGHT ? kL32LightBytes : kL32Bytes];
-    const crc32_gpu_pack_t *pk = reinterpret_cast<const crc32_gpu_pack_t *>(a.pack);
-    fill_lds32<LIGHT, kBlk32<LIGHT>>(lds_raw, pk);
-    __syncthreads();
-    const Tab32<LIGHT> lds{lds_raw};
-
-    constexpr int PPW = 64 >> LOG2G;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t gl = lane & ((1u << LOG2G) - 1u), grp = lane >> LOG2G;
-    const uint32_t lc0 = (lane & 31u) << 2, lc1 = lc0 | 0x10000u;
-    const uint32_t xorout = pk->xorout;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
-    const uint32_t nw = gridDim.x * kWavesPerBlock;
-
-    if (MODE == kOffsets) {
-        uint64_t first, last;
-        wave_range(a.offsets, a.count, wave, nw, &first, &last);
-        for (uint64_t p = first; p < last; p++) {
-            const uint64_t m0 = a.offsets[p], m1 = a.offsets[p + 1];
-            // message mode: a message shorter than its headers fails verification
-            const bool short_msg = a.msg && m1 - m0 < a.pay_off;
-            const uint64_t o = a.msg ? (short_msg ? m1 : m0 + a.pay_off) : m0;
-            const uint64_t n = m1 - o;
-            const uint32_t x = n < (1ull << 31) ? payload32_g64<NT>(lds, pk, a.base + o, n, gl, lc0, lc1)
-                                                : payload32_generic<LOG2G, NT>(lds, pk, a.base + o, n, gl, lc0, lc1);
-            if (gl == 0) {
-                if (VERIFY && a.msg) {
-                    const bool bad = short_msg || load_be32(a.base + m0 + a.hash_off) != (x ^ xorout);
-                    if (a.status) a.status[p] = bad ? 1 : 0;
-                    if (bad && a.mismatches) atomicAdd(a.mismatches, 1u);
-                } else {
-                    emit<uint32_t, VERIFY>(a, p, x ^ xorout);
-                }
-            }
-        }
-        return;
-    }
-    for (uint64_t pb = (uint64_t)wave * PPW; pb < a.count; pb += (uint64_t)nw * PPW) {
-        const uint64_t p = pb + grp;
-        const bool act = p < a.count;
-        const uint64_t pc = act ? p : a.count - 1;
-        uint32_t x;
-        if (MODE == kFixedAligned)
-            x = payload32_aligned<LOG2G, NT>(lds, a.base + pc * a.stride, a.len >> (4 + LOG2G), gl, lc0, lc1, pk->init);
-        else
-            x = payload32_generic<LOG2G, NT>(lds, pk, a.base + pc * a.stride, a.len, gl, lc0, lc1);
-        if (act && gl == 0) emit<uint32_t, VERIFY>(a, p, x ^ xorout);
-    }
-}
-
-// ----------------------------------------------------------------- CRC-64 --
-
-__device__ __forceinline__ uint64_t xor3_64(uint64_t a, uint64_t b, uint64_t c) {
-    return (uint64_t)xor3((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32)) << 32 |
-           xor3((uint32_t)a, (uint32_t)b, (uint32_t)c);
-}
-
-// XOR of 16 table words and one more value: 8 bitop3 per 32-bit half.
-__device__ __forceinline__ uint64_t xor17(const uint64_t *r, uint64_t extra) {
-    const uint64_t a = xor3_64(r[0], r[1], r[2]), b = xor3_64(r[3], r[4], r[5]), c = xor3_64(r[6], r[7], r[8]);
-    const uint64_t d = xor3_64(r[9], r[10], r[11]), e = xor3_64(r[12], r[13], r[14]);
-    return xor3_64(xor3_64(r[15], extra, a), xor3_64(b, c, d), e);
-}
-
-#ifndef MCK_SDWA64
-#define MCK_SDWA64 1
-#endif
-
-// Per-lane lookup address registers of f64x.  With SDWA (gfx9 sub-dword
-// operands) one v_and_b32_sdwa both extracts a nibble of byte b and places it:
-// the high nibble as (byte & 0xF0) -- its own address -- and the low nibble
-// into byte 1 of a persistent register whose byte 0 holds the lane copy offset
-// (dst_unused:UNUSED_PRESERVE keeps it), so a lookup costs one VALU op and no
-// separate masking.
-struct Lane64 {
-    uint32_t lc;
-    uint32_t al[4];
-};
-__device__ __forceinline__ Lane64 lane64(uint32_t lc) { return Lane64{lc, {lc, lc, lc, lc}}; }
-
-#define MCK_SDWA_HI(B)                                                                              \
-    __device__ __forceinline__ uint32_t sdwa_hi##B(uint32_t x) {                                    \
-        uint32_t r;                                                                                 \
-        asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD "         \
-            "src1_sel:BYTE_" #B : "=v"(r) : "s"(0xF0u), "v"(x));                                    \
-        return r;                                                                                   \
-    }                                                                                               \
-    __device__ __forceinline__ void sdwa_lo##B(uint32_t &a, uint32_t x) {                           \
-        asm("v_and_b32_sdwa %0, %1, %2 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD "   \
-            "src1_sel:BYTE_" #B : "+v"(a) : "s"(0x0Fu), "v"(x));                                    \
-    }
-MCK_SDWA_HI(0)
-MCK_SDWA_HI(1)
-MCK_SDWA_HI(2)
-MCK_SDWA_HI(3)
-#undef MCK_SDWA_HI
-
-template <int B>
-__device__ __forceinline__ uint32_t sdwa_hi(uint32_t x) {
-    if constexpr (B == 0) return sdwa_hi0(x);
-    else if constexpr (B == 1) return sdwa_hi1(x);
-    else if constexpr (B == 2) return sdwa_hi2(x);
-    else return sdwa_hi3(x);
-}
-template <int B>
-__device__ __forceinline__ void sdwa_lo(uint32_t &a, uint32_t x) {
-    if constexpr (B == 0) sdwa_lo0(a, x);
-    else if constexpr (B == 1) sdwa_lo1(a, x);
-    else if constexpr (B == 2) sdwa_lo2(a, x);
-    else sdwa_lo3(a, x);
-}
-
-template <int B>
-__device__ __forceinline__ void f64x_byte(const uint8_t *lds, uint32_t xl, uint32_t xh, Lane64 &ln, uint64_t *r) {
-#if MCK_SDWA64
-    sdwa_lo<B>(ln.al[B], xl);
-    r[4 * B + 0] = lds64(lds, ln.al[B] + B * 4096);
-    r[4 * B + 1] = lds64(lds, sdwa_hi<B>(xl) + kL64Hi + B * 256);
-    sdwa_lo<B>(ln.al[B], xh);
-    r[4 * B + 2] = lds64(lds, ln.al[B] + (B + 4) * 4096);
-    r[4 * B + 3] = lds64(lds, sdwa_hi<B>(xh) + kL64Hi + (B + 4) * 256);
-#else
-    const uint32_t sl = 0x0C0C0400u | ((uint32_t)B << 8);  // byte B -> address byte 1, lane byte -> 0
-    const uint32_t sh = 0x0C0C0C04u | (uint32_t)B;         // byte B -> address byte 0
-    const uint32_t l0 = xl & 0x0F0F0F0Fu, h0 = xl & 0xF0F0F0F0u;
-    const uint32_t l1 = xh & 0x0F0F0F0Fu, h1 = xh & 0xF0F0F0F0u;
-    r[4 * B + 0] = lds64(lds, __builtin_amdgcn_perm(l0, ln.lc, sl) + B * 4096);
-    r[4 * B + 1] = lds64(lds, __builtin_amdgcn_perm(h0, h0, sh) + kL64Hi + B * 256);
-    r[4 * B + 2] = lds64(lds, __builtin_amdgcn_perm(l1, ln.lc, sl) + (B + 4) * 4096);
-    r[4 * B + 3] = lds64(lds, __builtin_amdgcn_perm(h1, h1, sh) + kL64Hi + (B + 4) * 256);
-#endif
-}
-
-// Z^(16G)(x) ^ next from the 16 nibble tables (LDS map above): one VALU op per
-// lookup to form its address, 8 v_bitop3 per 32-bit half for the XOR tree.
-__device__ __forceinline__ uint64_t f64x(const uint8_t *lds, uint64_t x, uint64_t next, Lane64 &ln) {
-    const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
-    uint64_t r[16];
-    f64x_byte<0>(lds, xl, xh, ln, r);
-    f64x_byte<1>(lds, xl, xh, ln, r);
-    f64x_byte<2>(lds, xl, xh, ln, r);
-    f64x_byte<3>(lds, xl, xh, ln, r);
-    return xor17(r, next);
-}
-
-template <bool OG>
-__device__ __forceinline__ uint64_t op64(const uint8_t *lds, const crc64_gpu_pack_t *pk, uint32_t o, uint64_t x) {
-    uint64_t r[16];
-    if constexpr (OG) {
-        const uint64_t *t = &pk->ops[o][0][0];
-#pragma unroll
-        for (int h = 0; h < 16; h++) r[h] = t[h * 16 + ((x >> (4 * h)) & 15u)];
-    } else {
-        const uint32_t base = kL64Main + o * 2048;
-#pragma unroll
-        for (int h = 0; h < 16; h++) r[h] = lds64(lds, base + h * 128 + (uint32_t)(((x >> (4 * h)) & 15u) << 3));
-    }
-    return xor17(r, 0);
-}
-
-template <int LOG2G, bool OG>
-__device__ __forceinline__ uint64_t combine64(const uint8_t *lds, const crc64_gpu_pack_t *pk, uint64_t s0, uint64_t s1,
-                                              uint32_t gl) {
-    uint64_t x = s0 ^ op64<OG>(lds, pk, 0, s1);
-#pragma unroll
-    for (int k = 0; k < LOG2G; k++) {
-        const uint64_t other = __shfl_xor(x, 1 << k, 64);
-        const bool bit = (gl >> k) & 1u;
-        const uint64_t lo = bit ? other : x, hi = bit ? x : other;
-        x = lo ^ op64<OG>(lds, pk, 1 + k, hi);
-    }
-    return x;
-}
-
-template <int BLOCK, bool OG>
-__device__ void fill_lds64(uint8_t *lds, const crc64_gpu_pack_t *pk) {
-    uint64_t *l = reinterpret_cast<uint64_t *>(lds);
-    // low-nibble tables (main[2p]), 32 copies; high-nibble tables (main[2p+1]) at 16-B entry stride
-    for (uint32_t d = threadIdx.x; d < 4096u; d += BLOCK) l[d] = pk->main[2 * (d >> 9)][(d >> 5) & 15u];
-    for (uint32_t d = threadIdx.x; d < 128u; d += BLOCK) l[kL64Hi / 8 + (d >> 4) * 32 + (d & 15u) * 2] = pk->main[2 * (d >> 4) + 1][d & 15u];
-    if constexpr (!OG) {
-        const uint64_t *ops = &pk->ops[0][0][0];
-        const uint32_t nops = pk->nops * 256u;
-        for (uint32_t d = threadIdx.x; d < nops; d += BLOCK) l[kL64Main / 8 + d] = ops[d];
-    }
-}
-
-__device__ __forceinline__ uint64_t lo64(uint4 v) { return (uint64_t)v.y << 32 | v.x; }
-__device__ __forceinline__ uint64_t hi64(uint4 v) { return (uint64_t)v.w << 32 | v.z; }
-
-template <int LOG2G, bool NT, bool OG>
-__device__ __forceinline__ uint64_t payload64_aligned(const uint8_t *lds, const crc64_gpu_pack_t *pk, const uint8_t *p,
-                                                      uint32_t K, uint32_t gl, uint32_t lc, uint64_t init) {
-    constexpr int G = 1 << LOG2G;
-    constexpr int R = kRing;
-    Lane64 ln = lane64(lc);
-    const uint4 *src = reinterpret_cast<const uint4 *>(p) + gl;
-    uint4 ring[R];
-#pragma unroll
-    for (int u = 0; u < R; u++) ring[u] = (uint32_t)u < K ? ld16<NT>(src + (uint64_t)u * G) : make_uint4(0, 0, 0, 0);
-#if MCK_LA64
-    // x holds state ^ (the data word of the step about to run)
-    uint64_t x0 = (gl == 0 ? init : 0ull) ^ lo64(ring[0]), x1 = hi64(ring[0]);
-    uint32_t k = 0;
-    for (; k + 2 * R <= K; k += R) {  // every load and look-ahead in range
-#pragma unroll
-        for (int u = 0; u < R; u++) {
-            ring[u] = ld16<NT>(src + (uint64_t)(k + u + R) * G);
-            const uint4 nx = ring[(u + 1) % R];
-            x0 = f64x(lds, x0, lo64(nx), ln);
-            x1 = f64x(lds, x1, hi64(nx), ln);
-        }
-    }
-    for (; k < K; k += R) {
-#pragma unroll
-        for (int u = 0; u < R; u++) {
-            if (k + u + R < K) ring[u] = ld16<NT>(src + (uint64_t)(k + u + R) * G);
-            if (k + u < K) {
-                const uint4 nx = k + u + 1 < K ? ring[(u + 1) % R] : make_uint4(0, 0, 0, 0);
-                x0 = f64x(lds, x0, lo64(nx), ln);
-                x1 = f64x(lds, x1, hi64(nx), ln);
-            }
-        }
-    }
-#else
-    uint64_t x0 = gl == 0 ? init : 0ull, x1 = 0;
-    for (uint32_t k = 0; k < K; k += R) {
-#pragma unroll
-        for (int u = 0; u < R; u++) {
-            const uint4 v = ring[u];
-            const uint32_t kn = k + u + R;
-            if (kn < K) ring[u] = ld16<NT>(src + (uint64_t)kn * G);
-            if (k + u < K) {
-                x0 = f64x(lds, x0 ^ lo64(v), 0, ln);
-                x1 = f64x(lds, x1 ^ hi64(v), 0, ln);
-            }
-        }
-    }
-#endif
-    return combine64<LOG2G, OG>(lds, pk, x0, x1, gl);
-}
-
-template <int LOG2G, bool NT>
-__device__ __forceinline__ uint64_t payload64_generic(const uint8_t *lds, const crc64_gpu_pack_t *pk,
-                                                      const uint8_t *p, uint64_t len, uint32_t gl, uint32_t lc) {
-    constexpr int G = 1 << LOG2G;
-    constexpr int64_t step = 16 * G;
-    const uint64_t init = pk->init;
-    const uint64_t sa = reinterpret_cast<uint64_t>(p), ea = sa + len;
-    const uint64_t a0 = sa & ~15ull, a1 = (ea + 15) & ~15ull;
-    const int64_t W = (int64_t)(a1 - a0);
-    const int64_t K = (W + step - 1) >> (4 + LOG2G);
-    const int64_t r0 = W - K * step;
-    const int64_t hs = (int64_t)(sa - a0), he = (int64_t)(ea - a0);
-    const int64_t ilen = (int64_t)len;
-    const int64_t kmax = LOG2G == 6 ? K : wave_max(K);
-    const int64_t lane_off = 16 * (int64_t)gl;
-
-    auto fetch = [&](int64_t k) -> uint4 {
-        const int64_t pc = r0 + k * step + lane_off;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (k < K && pc >= 0) v = ld16<NT>(reinterpret_cast<const uint4 *>(a0 + (uint64_t)pc));
-        return v;
-    };
-    // edge handling (crc_gpu_mask.h) for the piece of step k < K
-    auto prep = [&](int64_t k, uint4 v, uint64_t *w0, uint64_t *w1) {
-        const int64_t pc = r0 + k * step + lane_off;
-        *w0 = lo64(v);
-        *w1 = hi64(v);
-        if (!mck_piece_clean(pc, hs, he, 8)) {
-            const int64_t lo = pc - hs;
-            *w0 = mck_mask64(*w0, lo, ilen, init);
-            *w1 = mck_mask64(*w1, lo + 8, ilen, init);
-        }
-    };
-
-    uint4 ring[kRing];
-#pragma unroll
-    for (int u = 0; u < kRing; u++) ring[u] = fetch(u);
-    uint64_t x0 = 0, x1 = 0;
-    Lane64 ln = lane64(lc);
-    for (int64_t k = 0; k < kmax; k += kRing) {
-#pragma unroll
-        for (int u = 0; u < kRing; u++) {
-            const int64_t j = k + u;
-            const uint4 raw = ring[u];
-            ring[u] = fetch(j + kRing);
-            if (j < K) {
-                uint64_t w0, w1;
-                prep(j, raw, &w0, &w1);
-                x0 = f64x(lds, x0 ^ w0, 0, ln);
-                x1 = f64x(lds, x1 ^ w1, 0, ln);
-            }
-        }
-    }
-    uint64_t x = combine64<LOG2G, false>(lds, pk, x0, x1, gl);
-    x = op64<false>(lds, pk, 1 + LOG2G + (uint32_t)(a1 - ea), x);
-    if (len < 8) x ^= pk->zinit[len];
-    return x;
-}
-
-// CRC-64 counterpart of payload32_g64.
-template <bool NT>
-__device__ __forceinline__ uint64_t payload64_g64(const uint8_t *lds, const crc64_gpu_pack_t *pk, const uint8_t *p,
-                                                  uint64_t len, uint32_t gl, uint32_t lc) {
-    const uint64_t init = pk->init;
-    const uint64_t sa = reinterpret_cast<uint64_t>(p), ea = sa + len;
-    const uint64_t a0 = sa & ~15ull, a1 = (ea + 15) & ~15ull;
-    const uint32_t W = (uint32_t)(a1 - a0);
-    const uint32_t K = (W + 1023u) >> 10;
-    const uint32_t lead = K * 1024u - W;
-    const uint8_t *wb = reinterpret_cast<const uint8_t *>(a0 - lead);
-    const uint32_t qs = lead + (uint32_t)(sa - a0);
-    const uint32_t qe = lead + (uint32_t)(ea - a0);
-    const int32_t ilen = (int32_t)len;
-    const uint32_t lo_lane = 16u * gl;
-    const uint32_t kc0 = (qs + 8u + 1023u) >> 10;
-    const uint32_t kc1 = qe >= 1024u ? (qe - 1024u) / 1024u + 1u : 0u;
-
-    auto fetch = [&](uint32_t k) -> uint4 {
-        const uint32_t q = k * 1024u + lo_lane;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (k < K && q >= lead) v = ld16<NT>(reinterpret_cast<const uint4 *>(wb + q));
-        return v;
-    };
-
-    uint64_t x0 = 0, x1 = 0;
-    Lane64 ln = lane64(lc);
-    uint4 ring[kRingOff];
-#pragma unroll
-    for (int u = 0; u < kRingOff; u++) ring[u] = fetch(u);
-    for (uint32_t k = 0; k < K; k += kRingOff) {
-#pragma unroll
-        for (int u = 0; u < kRingOff; u++) {
-            const uint4 v = ring[u];
-            const uint32_t kk = k + u;
-            ring[u] = fetch(kk + kRingOff);
-            if (kk < K) {
-                uint64_t w0 = lo64(v), w1 = hi64(v);
-                if (kk < kc0 || kk >= kc1) {
-                    const int32_t lo = (int32_t)(kk * 1024u + lo_lane) - (int32_t)qs;
-                    w0 = mck_mask64(w0, lo, ilen, init);
-                    w1 = mck_mask64(w1, lo + 8, ilen, init);
-                }
-                x0 = f64x(lds, x0 ^ w0, 0, ln);
-                x1 = f64x(lds, x1 ^ w1, 0, ln);
-            }
-        }
-    }
-    uint64_t x = combine64<6, false>(lds, pk, x0, x1, gl);
-    x = op64<false>(lds, pk, 1 + 6 + (uint32_t)(a1 - ea), x);
-    if (len < 8) x ^= pk->zinit[len];
-    return x;
-}
-
-template <int LOG2G, int MODE, bool VERIFY, bool NT>
-__global__ __launch_bounds__(kBlk64<MODE>, kWpe64<MODE>) void crc64_batch_kernel(BatchArgs a) {
-    using S = Shape<64, MODE>;
-    constexpr int kWPB = S::block / 64;
-    __shared__ __attribute__((aligned(16))) uint8_t lds[S::lds64_bytes];
-    const crc64_gpu_pack_t *pk = reinterpret_cast<const crc64_gpu_pack_t *>(a.pack);
-    fill_lds64<S::block, S::ops_global>(lds, pk);
-    __syncthreads();
-
-    constexpr int PPW = 64 >> LOG2G;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t gl = lane & ((1u << LOG2G) - 1u), grp = lane >> LOG2G;
-    const uint32_t lc = (lane & 31u) << 3;
-    const uint64_t xorout = pk->xorout;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWPB + (threadIdx.x >> 6));
-    const uint32_t nw = gridDim.x * kWPB;
-
-    if (MODE == kOffsets) {
-        uint64_t first, last;
-        wave_range(a.offsets, a.count, wave, nw, &first, &last);
-        for (uint64_t p = first; p < last; p++) {
-            const uint64_t o = a.offsets[p];
-            const uint64_t n = a.offsets[p + 1] - o;
-            const uint64_t x = n < (1ull << 31) ? payload64_g64<NT>(lds, pk, a.base + o, n, gl, lc)
-                                                : payload64_generic<LOG2G, NT>(lds, pk, a.base + o, n, gl, lc);
-            if (gl == 0) emit<uint64_t, VERIFY>(a, p, x ^ xorout);
-        }
-        return;
-    }
-    for (uint64_t pb = (uint64_t)wave * PPW; pb < a.count; pb += (uint64_t)nw * PPW) {
-        const uint64_t p = pb + grp;
-        const bool act = p < a.count;
-        const uint64_t pc = act ? p : a.count - 1;
-        uint64_t x;
-        if (MODE == kFixedAligned)
-            x = payload64_aligned<LOG2G, NT, S::ops_global>(lds, pk, a.base + pc * a.stride, (uint32_t)(a.len >> (4 + LOG2G)), gl, lc, pk->init);
-        else
-            x = payload64_generic<LOG2G, NT>(lds, pk, a.base + pc * a.stride, a.len, gl, lc);
-        if (act && gl == 0) emit<uint64_t, VERIFY>(a, p, x ^ xorout);
-    }
-}
-
+namespace mck {
 // ------------------------------------------------------------ host side ----
 
 thread_local char t_err[256] = "";
 
-int set_err(int rc, const char *fmt, const char *a = "", int b = 0) {
+int set_err(int rc, const char *fmt, const char *a, int b) {
     snprintf(t_err, sizeof(t_err), fmt, a, b);
     return rc;
 }
@@ -847,14 +50,6 @@ int hip_err(hipError_t e, const char *what) {
     snprintf(t_err, sizeof(t_err), "%s: %s", what, hipGetErrorString(e));
     return MCHECKSUM_GPU_EHIP;
 }
-
-constexpr int kMaxDev = 64;
-
-struct DevCtx {
-    bool init = false;
-    int cus = 0;
-    void *pack[MCK_NMODELS][CRC_GPU_MAX_LOG2G + 1] = {};
-};
 
 std::mutex g_mu;
 DevCtx g_dev[kMaxDev];
@@ -927,6 +122,13 @@ int get_pack(DevCtx *c, int idx, int log2g, const void **pack) {
     return 0;
 }
 
+typedef void (*kern_t)(BatchArgs);
+
+struct KLaunch {
+    kern_t k;
+    int block, blocks_per_cu;
+};
+
 int choose_log2g(size_t len) {
     const char *env = getenv("MCHECKSUM_GPU_LOG2G");
     if (env && env[0]) {
@@ -939,13 +141,6 @@ int choose_log2g(size_t len) {
     while (lg < CRC_GPU_MAX_LOG2G && ((size_t)1 << (lg + 1)) <= target) lg++;
     return lg;
 }
-
-typedef void (*kern_t)(BatchArgs);
-
-struct KLaunch {
-    kern_t k;
-    int block, blocks_per_cu;
-};
 
 template <int W, int LOG2G, int MODE, bool VERIFY, bool NT = false, bool LIGHT = false>
 KLaunch kernel_ptr() {
@@ -1099,7 +294,9 @@ int launch_fixed(DevCtx *c, const void *pack, int width, int lg, const void *dev
     return launch(k, a, grid_for(c, (count + ppw - 1) / ppw, k), stream);
 }
 
-}  // namespace
+}  // namespace mck
+
+using namespace mck;
 
 extern "C" {
 

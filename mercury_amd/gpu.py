@@ -158,6 +158,91 @@ def verify_messages(data: torch.Tensor, msg_offsets: torch.Tensor, payload_offse
     return status, mism
 
 
+class SegmentBatch:
+    """A scatter-gather batch prepared once: object j = the concatenation of
+    segments[obj_first[j]:obj_first[j+1]] (default: one object), each segment a
+    contiguous 1-D uint8 device tensor (views of larger buffers are fine) --
+    the bulk-handle shape, HG_Bulk_create's (buf_ptrs, buf_sizes) in device
+    memory.  The segment table and the scan workspace stay on the device, so
+    `checksum` is one C-ABI call (no host work per launch).  Keep the segment
+    tensors alive while the batch is in use."""
+
+    def __init__(self, segments, obj_first=None, device=None):
+        import numpy as np
+        addr, lens, dev = [], [], device
+        for t in segments:
+            _check_device_u8(t, "segment")
+            if t.dim() != 1:
+                raise GpuChecksumError("segments must be 1-D byte tensors")
+            dev = t.device if dev is None else dev
+            if t.device != dev:
+                raise GpuChecksumError("segments must share one device")
+            addr.append(t.data_ptr())
+            lens.append(t.numel())
+        self.nseg = len(addr)
+        first = np.asarray([0, self.nseg] if obj_first is None else obj_first, dtype=np.int64)
+        if first.ndim != 1 or len(first) < 1 or np.any(first[1:] < first[:-1]) or first[0] < 0 \
+                or first[-1] > self.nseg:
+            raise GpuChecksumError("obj_first must be non-decreasing indices into segments")
+        self.nobj = len(first) - 1
+        self.device = dev if dev is not None else torch.device("cuda", torch.cuda.current_device())
+        self.bytes = int(np.sum(np.asarray(lens, dtype=np.int64)[first[0]:first[-1]])) if self.nseg else 0
+        self.meta = torch.from_numpy(np.concatenate([np.asarray(addr, dtype=np.uint64).view(np.int64),
+                                                     np.asarray(lens, dtype=np.int64), first])).to(self.device)
+        self.work = torch.empty((_lib().mchecksum_gpu_segments_work_size(self.nseg) + 7) // 8, dtype=torch.int64,
+                                device=self.device)
+
+    def checksum(self, method: str, out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+        if out is None:
+            out = torch.empty(self.nobj, dtype=out_dtype(method), device=self.device)
+        elif out.numel() < self.nobj or out.dtype != out_dtype(method) or not out.is_cuda:
+            raise GpuChecksumError("out tensor has the wrong size, dtype or device")
+        base, n = self.meta.data_ptr(), self.nseg
+        rc = _lib().mchecksum_gpu_checksum_segments(method.encode(), base, base + 8 * n, n, base + 16 * n,
+                                                    self.nobj, self.work.data_ptr(), self.work.numel() * 8,
+                                                    out.data_ptr(), _stream_handle(stream))
+        if rc != 0:
+            _err(rc, "mchecksum_gpu_checksum_segments")
+        return out
+
+
+def checksum_segments(method: str, segments, obj_first=None, out: torch.Tensor | None = None,
+                      stream=None) -> torch.Tensor:
+    """One-shot SegmentBatch(segments, obj_first).checksum(method)."""
+    b = SegmentBatch(segments, obj_first)
+    out = b.checksum(method, out, stream)
+    # the batch's device table and workspace are freed on return: the caching
+    # allocator orders their reuse after this launch on the current stream;
+    # another stream must be recorded
+    if stream is not None:
+        if isinstance(stream, torch.cuda.Stream):
+            b.meta.record_stream(stream)
+            b.work.record_stream(stream)
+        else:
+            torch.cuda.synchronize(b.device)
+    return out
+
+
+def verify_core_headers(data: torch.Tensor, msg_offsets: torch.Tensor, kind: str = "request",
+                        method: str = "crc16", stream=None, offsets_host=None):
+    """Check the CRC16 of each message's 16-byte Mercury core header
+    (kind "request" or "response").  Returns (status uint8 per message, count)."""
+    from ._lib import CORE_HEADER_REQUEST, CORE_HEADER_RESPONSE
+    k = {"request": CORE_HEADER_REQUEST, "response": CORE_HEADER_RESPONSE}.get(kind)
+    if k is None:
+        raise GpuChecksumError("kind must be 'request' or 'response'")
+    _check_device_u8(data, "data")
+    _check_offsets(data, msg_offsets, offsets_host)
+    count = msg_offsets.numel() - 1
+    status = torch.empty(max(count, 0), dtype=torch.uint8, device=data.device)
+    mism = torch.zeros(1, dtype=torch.int32, device=data.device)
+    rc = _lib().mchecksum_gpu_verify_core_headers(method.encode(), k, data.data_ptr(), msg_offsets.data_ptr(), count,
+                                                  status.data_ptr(), mism.data_ptr(), _stream_handle(stream))
+    if rc != 0:
+        _err(rc, "mchecksum_gpu_verify_core_headers")
+    return status, mism
+
+
 def fill_splitmix(t: torch.Tensor, seed: int, first_word: int = 0, stream=None) -> torch.Tensor:
     """Fill a device tensor with the synthetic payload bytes of SURVEY.md 8(d)."""
     _check_device_u8(t, "tensor")

@@ -37,3 +37,10 @@ def varlen_offsets(seed: int, count: int, min_len: int = 64, max_len: int = 6553
     off = np.zeros(count + 1, dtype=np.uint64)
     np.cumsum(varlen_lengths(seed, count, min_len, max_len), out=off[1:])
     return off
+
+
+def segment_slots(seed: int, nseg: int) -> np.ndarray:
+    """Bulk-segment layout (bench config "seg"): segment s of the batch lives in
+    slot slots[s] of the buffer -- a seeded permutation, so an object's
+    segments are scattered rather than adjacent."""
+    return np.random.default_rng(seed & _M64).permutation(nseg)

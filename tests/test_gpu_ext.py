@@ -1,0 +1,192 @@
+"""GPU parity of the 8(f) entry points (mchecksum_gpu_ext.hip) through the C ABI.
+
+* checksum_segments: scatter-gather objects (a bulk handle's segment list,
+  HG_Bulk_create(count, buf_ptrs, buf_sizes), src/mercury_bulk.h:55) -- the
+  value must equal the oracle CRC of the concatenated bytes and the streaming
+  API fed one update per segment.
+* verify_core_headers: Mercury core headers encoded as
+  hg_core_header_request_proc / _response_proc do it
+  (src/mercury_core_header.c:175-289), hashed with the streaming API over the
+  host-order field values, then corrupted in known places.
+"""
+import struct
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _host(t):
+    return t.cpu().numpy()
+
+
+@pytest.fixture
+def buf(gpu):
+    import torch
+    n = 24 << 20
+    t = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    gpu.fill_splitmix(t, 0x5E6)
+    return t
+
+
+def _objects(rng, buf_len, nobj, max_seg=6, lens=None):
+    """Random segment views (offset, length) grouped into objects."""
+    segs, first = [], [0]
+    pool = lens or [0, 1, 3, 7, 8, 15, 16, 17, 63, 64, 100, 1000, 4095, 4096, 4097, 65536, 100003, 262143, 262144,
+                    262145, 600000, 1 << 20, (1 << 20) + 5]
+    for _ in range(nobj):
+        for _ in range(int(rng.integers(0, max_seg + 1))):
+            ln = int(pool[int(rng.integers(0, len(pool)))])
+            off = int(rng.integers(0, buf_len - ln))
+            segs.append((off, ln))
+        first.append(len(segs))
+    return segs, first
+
+
+def _want(oracle_mod, method, host, segs, first):
+    out = []
+    for j in range(len(first) - 1):
+        b = b"".join(host[o:o + n].tobytes() for o, n in segs[first[j]:first[j + 1]])
+        out.append(oracle_mod.crc(method, np.frombuffer(b, dtype=np.uint8)))
+    return out
+
+
+@pytest.mark.parametrize("method", ["crc32c", "crc64"])
+def test_segments_random_objects(gpu, buf, oracle_mod, method):
+    rng = np.random.default_rng(77 if method == "crc32c" else 78)
+    host = _host(buf)
+    segs, first = _objects(rng, buf.numel() - 64, 120)
+    views = [buf[o:o + n] for o, n in segs]
+    got = gpu.as_unsigned(gpu.checksum_segments(method, views, first))
+    assert got.tolist() == _want(oracle_mod, method, host, segs, first)
+
+
+@pytest.mark.parametrize("method", ["crc32c", "crc64"])
+def test_segments_one_huge_segment_and_chunk_edges(gpu, buf, oracle_mod, method):
+    """One 20 MiB segment (80 chunks) and objects whose segment lengths sit on
+    and around the 256 KiB chunk size."""
+    host = _host(buf)
+    big = [(3, 20 << 20)]
+    got = gpu.as_unsigned(gpu.checksum_segments(method, [buf[3:3 + (20 << 20)]]))
+    assert got.tolist() == _want(oracle_mod, method, host, big, [0, 1])
+    k = 256 << 10
+    segs = [(11, k - 1), (5000, k), (9, k + 1), (77, 2 * k), (1 << 20, 3 * k + 13), (0, 0), (123, 1)]
+    first = [0, 1, 2, 3, 4, 5, 7, 7]
+    got = gpu.as_unsigned(gpu.checksum_segments(method, [buf[o:o + n] for o, n in segs], first))
+    assert got.tolist() == _want(oracle_mod, method, host, segs, first)
+
+
+def test_segments_match_streaming_api_and_edges(gpu, buf):
+    """Per-segment mchecksum_update (what a host would do) equals the GPU value;
+    empty objects give the CRC of the empty message; segments outside
+    [first[0], first[-1]) are ignored."""
+    from mercury_amd import Checksum
+    host = _host(buf)
+    rng = np.random.default_rng(5)
+    segs, first = _objects(rng, 1 << 20, 30, lens=[0, 1, 2, 5, 9, 31, 200, 5000, 70000])
+    for method in ("crc32c", "crc64"):
+        got = gpu.as_unsigned(gpu.checksum_segments(method, [buf[o:o + n] for o, n in segs], first))
+        for j in range(len(first) - 1):
+            ck = Checksum(method)
+            for o, n in segs[first[j]:first[j + 1]]:
+                ck.update(host[o:o + n].tobytes())
+            assert int(got[j]) == ck.get()
+        # objects over a sub-range of the list
+        sub = [3, 5, 5, 9]
+        got2 = gpu.as_unsigned(gpu.checksum_segments(method, [buf[o:o + n] for o, n in segs], sub))
+        for j in range(len(sub) - 1):
+            ck = Checksum(method)
+            for o, n in segs[sub[j]:sub[j + 1]]:
+                ck.update(host[o:o + n].tobytes())
+            assert int(got2[j]) == ck.get()
+    empty = gpu.as_unsigned(gpu.checksum_segments("crc32c", [], [0, 0, 0]))
+    assert empty.tolist() == [Checksum("crc32c").get()] * 2
+
+
+def test_segments_reject_bad_arguments(gpu, buf):
+    with pytest.raises(gpu.GpuChecksumError):
+        gpu.checksum_segments("crc32c", [buf[:10]], [0, 2])
+    with pytest.raises(gpu.GpuChecksumError):
+        gpu.checksum_segments("crc16", [buf[:10]])  # no GPU segment kernel for 16-bit models
+    L = gpu._lib()
+    rc = L.mchecksum_gpu_checksum_segments(b"crc32c", buf.data_ptr(), buf.data_ptr(), 4, buf.data_ptr(), 1,
+                                           buf.data_ptr(), 8, buf.data_ptr(), None)
+    assert rc == -1  # workspace smaller than mchecksum_gpu_segments_work_size(4)
+
+
+# ------------------------------------------------------------ core headers --
+
+def _request(rng, ck):
+    hg, proto, rid, flags, cookie = 0x48 | 0x47, 5, int(rng.integers(0, 2**63)), int(rng.integers(0, 256)), \
+        int(rng.integers(0, 256))
+    ck.reset()
+    for f in (struct.pack("<B", hg), struct.pack("<B", proto), struct.pack("<Q", rid), struct.pack("<B", flags),
+              struct.pack("<B", cookie)):
+        ck.update(f)  # HG_CORE_HEADER_CHECKSUM_UPDATE: host-order values
+    h = ck.get()
+    wire = struct.pack(">BBQBBH", hg, proto, rid, flags, cookie, h) + b"\0\0"  # hash union is 4 bytes
+    assert len(wire) == 16
+    return wire
+
+
+def _response(rng, ck):
+    ret, flags, cookie = int(rng.integers(-128, 128)), int(rng.integers(0, 256)), int(rng.integers(0, 65536))
+    ck.reset()
+    for f in (struct.pack("<b", ret), struct.pack("<B", flags), struct.pack("<H", cookie)):
+        ck.update(f)
+    h = ck.get()
+    wire = struct.pack(">bBHH", ret, flags, cookie, h) + b"\0" * 10  # pad is never proc'd: hash lands at 4
+    assert len(wire) == 16
+    return wire
+
+
+@pytest.mark.parametrize("variant", [None, "crc16-arc", "crc16-ibm-3740"])
+@pytest.mark.parametrize("kind", ["request", "response"])
+def test_core_headers(gpu, kind, variant, monkeypatch):
+    import torch
+    from mercury_amd import Checksum
+    if variant:
+        monkeypatch.setenv("MCHECKSUM_CRC16_VARIANT", variant)
+    rng = np.random.default_rng(31 if kind == "request" else 32)
+    ck = Checksum("crc16")
+    msgs = []
+    for i in range(3000):
+        hdr = (_request if kind == "request" else _response)(rng, ck)
+        body = rng.integers(0, 256, size=int(rng.integers(0, 300)), dtype=np.uint8).tobytes()
+        msgs.append(bytearray(hdr + body))
+    hash_at = 12 if kind == "request" else 4
+    flips = {7: 1, 100: hash_at, 101: hash_at + 1, 2500: 0, 2999: 3}   # covered bytes -> must fail
+    quiet = {50: 14 if kind == "request" else 8}                        # pad byte -> must pass
+    for i, b in list(flips.items()) + list(quiet.items()):
+        msgs[i][b] ^= 0x10
+    msgs[1234] = msgs[1234][:15]                                       # shorter than the header
+    off = np.zeros(len(msgs) + 1, dtype=np.uint64)
+    off[1:] = np.cumsum([len(m) for m in msgs])
+    data = torch.zeros(int(off[-1]) + 64, dtype=torch.uint8, device="cuda")
+    data[:int(off[-1])].copy_(torch.from_numpy(np.frombuffer(b"".join(msgs), dtype=np.uint8).copy()))
+    status, mism = gpu.verify_core_headers(data, torch.from_numpy(off.astype(np.int64)).cuda(), kind=kind,
+                                           offsets_host=off)
+    bad = sorted(np.nonzero(status.cpu().numpy())[0].tolist())
+    assert bad == sorted(list(flips) + [1234])
+    assert int(mism.item()) == len(flips) + 1
+
+
+def test_core_header_values_pinned_to_oracle(oracle_mod):
+    """The encoder above hashes host-order images; pin one against the oracle
+    (default crc16 = CRC-16/T10-DIF, parity unpinned vs upstream mchecksum)."""
+    from mercury_amd import Checksum
+    img = struct.pack("<BBQBB", 0x4F, 5, 0x0123456789ABCDEF, 0x81, 0x22)
+    ck = Checksum("crc16")
+    ck.update(img)
+    assert ck.get() == oracle_mod.crc("crc16", np.frombuffer(img, dtype=np.uint8))
+
+
+def test_core_headers_reject_wide_methods(gpu):
+    import torch
+    data = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    offs = torch.tensor([0, 16], dtype=torch.int64, device="cuda")
+    with pytest.raises(gpu.GpuChecksumError):
+        gpu.verify_core_headers(data, offs, method="crc32c")
+    with pytest.raises(gpu.GpuChecksumError):
+        gpu.verify_core_headers(data, offs, kind="reply")

@@ -37,3 +37,15 @@ def test_sanitized_cpu_build(san):
     subprocess.run(["gcc", "-O1", "-g", "-std=c11", "-fno-omit-frame-pointer", "-fsanitize=" + san,
                     "-fno-sanitize-recover=all", *INC, TEST, *CPU_SRC, "-o", exe, "-lpthread"], check=True)
     _run(exe, {"MCHECKSUM_LOG_LEVEL": "none"})
+
+
+def test_scatter_gather_algebra():
+    """Host half of mchecksum_gpu_checksum_segments: shift tables and the
+    chunk-combine formula vs the streaming API (tests/native/test_shift_combine.c)."""
+    os.makedirs(OUT, exist_ok=True)
+    exe = os.path.join(OUT, "test_shift_combine")
+    src = os.path.join(ROOT, "tests", "native", "test_shift_combine.c")
+    subprocess.run(["gcc", "-O2", "-std=c11", "-Wall", *INC, src, *CPU_SRC, "-o", exe, "-lpthread"], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "all checks passed" in r.stdout

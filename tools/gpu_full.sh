@@ -7,7 +7,7 @@ O="$R/gpurun_out"
 step() { echo "== $1"; }
 step pytest
 timeout -k 10 700 python -m pytest tests -m gpu -x -q > $O/pytest_gpu.log 2>&1; rc=$?; tail -4 $O/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
-for c in ${CONFIGS:-metric c2 c3 c4}; do
+for c in ${CONFIGS:-metric c2 c3 c4 seg}; do
   step "bench $c"
   timeout -k 10 300 python bench.py --config $c > $O/bench_$c.json 2> $O/bench_$c.err || { tail -20 $O/bench_$c.err; exit 1; }
   cat $O/bench_$c.json
@@ -20,8 +20,8 @@ done
 cd /tmp && export TMPDIR=/tmp
 step "kernel trace"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_metric -o bench -- python3 $R/bench.py > $O/prof_bench.json 2> $O/prof_bench.err || { tail $O/prof_bench.err; exit 1; }
-for c in ${PMC_CONFIGS:-metric c2 c3 c4}; do
-  k=crc32c_batch_kernel; [ $c = c3 ] && k=crc64_batch_kernel
+for c in ${PMC_CONFIGS:-metric c2 c3 c4 seg}; do
+  k=crc32c_batch_kernel; [ $c = c3 ] && k=crc64_batch_kernel; [ $c = seg ] && k=seg_kernel
   step "pmc fetch/write $c"
   timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch_$c -o pmc -- python3 $R/bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline > $O/pmc_fetch_$c.json 2> $O/pmc_fetch_$c.err || { tail $O/pmc_fetch_$c.err; exit 1; }
   timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write_$c -o pmc -- python3 $R/bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline > $O/pmc_write_$c.json 2> $O/pmc_write_$c.err || { tail $O/pmc_write_$c.err; exit 1; }
