@@ -55,9 +55,10 @@ $(LIBDIR)/libmchecksum_cpu.so: $(COBJS) | $(LIBDIR)
 
 # Disassembly for roofline/occupancy inspection.
 asm: | $(BUILD)
-	$(HIPCC) $(HIPFLAGS) $(EXTRA_HIPFLAGS) $(INC) --save-temps -c $(CSRC)/mchecksum_gpu.hip -o $(BUILD)/asm_tmp.o \
-	  -Rpass-analysis=kernel-resource-usage 2> $(BUILD)/resource_usage.txt; \
-	mv mchecksum_gpu-hip-amdgcn-amd-amdhsa-$(ARCH).s $(BUILD)/ 2>/dev/null; rm -f mchecksum_gpu-hip-*; true
+	cd $(BUILD) && $(HIPCC) $(HIPFLAGS) $(EXTRA_HIPFLAGS) -I../include -I../$(CSRC) --save-temps \
+	  -c ../$(CSRC)/mchecksum_gpu.hip -o asm_tmp.o \
+	  -Rpass-analysis=kernel-resource-usage 2> resource_usage.txt; \
+	rm -f mchecksum_gpu-host-* mchecksum_gpu.hip-hip-*; true
 
 clean:
 	rm -rf $(BUILD) $(LIBDIR)/*.so
