@@ -78,11 +78,17 @@ variants: $(COBJS) $(BUILD)/mchecksum_gpu_ext.o | $(BUILD)
 	done
 .PHONY: variants
 
-# The committed kernel source at $(PREV) as variant "prev" (A/B against the last commit).
+# The committed kernel sources at $(PREV) (all of csrc/ and include/) as
+# variant "prev" (A/B against the last commit).
 PREV ?= HEAD
 prev: $(COBJS) | $(BUILD)
-	mkdir -p $(BUILD)/variants
-	git show $(PREV):mercury_amd/csrc/mchecksum_gpu.hip > $(BUILD)/variants/prev_gpu.hip
-	$(HIPCC) $(HIPFLAGS) $(INC) -I$(CSRC) -c $(BUILD)/variants/prev_gpu.hip -o $(BUILD)/variants/gpu_prev.o
-	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $(BUILD)/variants/libmchecksum_prev.so $(COBJS) $(BUILD)/variants/gpu_prev.o -lpthread
+	rm -rf $(BUILD)/variants/prev_src && mkdir -p $(BUILD)/variants/prev_src
+	git archive $(PREV) mercury_amd/csrc include | tar -x -C $(BUILD)/variants/prev_src
+	$(HIPCC) $(HIPFLAGS) -I$(BUILD)/variants/prev_src/include -I$(BUILD)/variants/prev_src/$(CSRC) \
+	  -c $(BUILD)/variants/prev_src/$(CSRC)/mchecksum_gpu.hip -o $(BUILD)/variants/gpu_prev.o
+	$(HIPCC) $(HIPFLAGS) -I$(BUILD)/variants/prev_src/include -I$(BUILD)/variants/prev_src/$(CSRC) \
+	  -c $(BUILD)/variants/prev_src/$(CSRC)/mchecksum_gpu_ext.hip -o $(BUILD)/variants/gpu_ext_prev.o
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $(BUILD)/variants/libmchecksum_prev.so $(COBJS) \
+	  $(BUILD)/variants/gpu_prev.o $(BUILD)/variants/gpu_ext_prev.o -lpthread
+	cp $(LIB) $(BUILD)/variants/libmchecksum_cur.so
 .PHONY: variants prev

@@ -40,9 +40,13 @@ CONFIGS = {
     # 8(f) 2: C3's bytes as bulk-handle segment lists -- 8192 objects x 4
     # segments of 256 KiB scattered over the buffer (permuted slots)
     "seg": ("crc64", 8192, 1 << 20, 0x4D43310000000003, "segments"),
+    # C5: the 2^20 x 64 KiB global batch (64 GiB) split over the ranks --
+    # strong scaling (8 GiB per GPU at 8 GPUs; all of it on one GPU at N=1)
+    "c5": ("crc32c", 1 << 20, 65536, 0x4D43310000000005, "fixed"),
     # BASELINE configs[0]: host CPU, through the drop-in streaming API
     "c1": ("crc32c", 1024, 4096, 0x4D43310000000001, "cpu"),
 }
+STRONG = {"c5"}  # configs whose count is the GLOBAL batch (split over ranks)
 
 
 def parse():
@@ -83,6 +87,9 @@ def main():
     from mercury_amd.shard import fixed_shard
 
     method, count, length, seed, layout = CONFIGS[args.config]
+    strong = args.config in STRONG
+    if strong:
+        count = fixed_shard(rank, world, count)[1]  # equal shards of the global batch
     stream = torch.cuda.current_stream()
     G.prepare(method)
 
@@ -179,7 +186,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(wall_max / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (splitmix64 bytes generated on device)",

@@ -78,10 +78,19 @@ constexpr uint32_t kL64Bytes = kL64Main + CRC64_NOPS_MAX * 2048;
 #define MCK_LA64 1
 #endif
 
+// Two workgroups per CU on the CRC-64 offsets path as well, with a 4-deep ring
+// so its loop fits 64 VGPRs: C4-layout CRC-64 +10% over one workgroup with
+// ring 8 (a ring of 8 at two workgroups spills: -42%; ring 4 on the CRC-32C
+// offsets path: -3%) -- profiles/r01/ab11_crc64_offsets_two.log.
+#ifndef MCK_CRC64_OFF_TWO
+#define MCK_CRC64_OFF_TWO 1
+#endif
+constexpr int kRingOff64 = MCK_CRC64_OFF_TWO ? 4 : kRingOff;
+
 template <int W, int MODE, bool LIGHT = false>
 struct Shape {
     static constexpr bool ops_global = W == 64 && MODE == 0 && MCK_CRC64_SPLIT;  // 0 = kFixedAligned
-    static constexpr bool two = W == 64 && MODE == 0;
+    static constexpr bool two = W == 64 && (MODE == 0 || (MODE == 2 && MCK_CRC64_OFF_TWO));
     static constexpr int block = LIGHT ? kLightBlock : two ? MCK_BLOCK64 : kBlock;
     static constexpr int blocks_per_cu = LIGHT ? 8 : two ? 2 : 1;
     static constexpr uint32_t lds64_bytes = ops_global ? kL64Main : kL64Bytes;
@@ -194,22 +203,27 @@ __device__ __forceinline__ uint32_t combine32(TAB lds, uint32_t s0, uint32_t s1,
     return x;
 }
 
+// LDS fill in 16-byte granules: a replicated entry's 4 neighbouring copies are
+// one ds_write_b128 of the same value (8 per thread at 1024 threads instead of
+// 32 dword loads + writes); the operator tables are copied as uint4.
 template <bool LIGHT, int BLOCK>
 __device__ void fill_lds32(uint8_t *lds, const crc32_gpu_pack_t *pk) {
-    uint32_t *l = reinterpret_cast<uint32_t *>(lds);
+    uint4 *l4 = reinterpret_cast<uint4 *>(lds);
     if constexpr (LIGHT) {
-        const uint32_t *m = &pk->main[0][0];
-        for (uint32_t d = threadIdx.x; d < 1024u; d += BLOCK) l[d] = m[d];
+        const uint4 *m = reinterpret_cast<const uint4 *>(&pk->main[0][0]);
+        for (uint32_t q = threadIdx.x; q < 256u; q += BLOCK) l4[q] = m[q];
     } else {
-        for (uint32_t d = threadIdx.x; d < 32768u; d += BLOCK) {
+        for (uint32_t q = threadIdx.x; q < 8192u; q += BLOCK) {
+            const uint32_t d = q << 2;
             const uint32_t region = d >> 14, e = (d >> 6) & 255u, half = (d >> 5) & 1u;
-            l[d] = pk->main[2 * region + half][e];
+            const uint32_t v = pk->main[2 * region + half][e];
+            l4[q] = make_uint4(v, v, v, v);
         }
     }
-    const uint32_t *ops = &pk->ops[0][0][0];
-    const uint32_t nops = pk->nops * 128u;
-    const uint32_t base = (LIGHT ? kL32LightMain : kL32Main) / 4;
-    for (uint32_t d = threadIdx.x; d < nops; d += BLOCK) l[base + d] = ops[d];
+    const uint4 *ops = reinterpret_cast<const uint4 *>(&pk->ops[0][0][0]);
+    const uint32_t nops = pk->nops * 32u;
+    const uint32_t base = (LIGHT ? kL32LightMain : kL32Main) / 16;
+    for (uint32_t q = threadIdx.x; q < nops; q += BLOCK) l4[base + q] = ops[q];
 }
 
 // Ring slot j % kRing holds the piece of step j, loaded kRing steps ahead.
@@ -593,13 +607,19 @@ __device__ __forceinline__ uint64_t combine64(const uint8_t *lds, const crc64_gp
 template <int BLOCK, bool OG>
 __device__ void fill_lds64(uint8_t *lds, const crc64_gpu_pack_t *pk) {
     uint64_t *l = reinterpret_cast<uint64_t *>(lds);
-    // low-nibble tables (main[2p]), 32 copies; high-nibble tables (main[2p+1]) at 16-B entry stride
-    for (uint32_t d = threadIdx.x; d < 4096u; d += BLOCK) l[d] = pk->main[2 * (d >> 9)][(d >> 5) & 15u];
+    uint4 *l4 = reinterpret_cast<uint4 *>(lds);
+    // low-nibble tables (main[2p]), 32 copies (two per ds_write_b128);
+    // high-nibble tables (main[2p+1]) at 16-B entry stride
+    for (uint32_t q = threadIdx.x; q < 2048u; q += BLOCK) {
+        const uint32_t d = q << 1;
+        const uint64_t v = pk->main[2 * (d >> 9)][(d >> 5) & 15u];
+        l4[q] = make_uint4((uint32_t)v, (uint32_t)(v >> 32), (uint32_t)v, (uint32_t)(v >> 32));
+    }
     for (uint32_t d = threadIdx.x; d < 128u; d += BLOCK) l[kL64Hi / 8 + (d >> 4) * 32 + (d & 15u) * 2] = pk->main[2 * (d >> 4) + 1][d & 15u];
     if constexpr (!OG) {
-        const uint64_t *ops = &pk->ops[0][0][0];
-        const uint32_t nops = pk->nops * 256u;
-        for (uint32_t d = threadIdx.x; d < nops; d += BLOCK) l[kL64Main / 8 + d] = ops[d];
+        const uint4 *ops = reinterpret_cast<const uint4 *>(&pk->ops[0][0][0]);
+        const uint32_t nops = pk->nops * 128u;
+        for (uint32_t q = threadIdx.x; q < nops; q += BLOCK) l4[kL64Main / 16 + q] = ops[q];
     }
 }
 
@@ -744,15 +764,15 @@ __device__ __forceinline__ uint64_t payload64_g64(const uint8_t *lds, const crc6
 
     uint64_t x0 = 0, x1 = 0;
     Lane64 ln = lane64(lc);
-    uint4 ring[kRingOff];
+    uint4 ring[kRingOff64];
 #pragma unroll
-    for (int u = 0; u < kRingOff; u++) ring[u] = fetch(u);
-    for (uint32_t k = 0; k < K; k += kRingOff) {
+    for (int u = 0; u < kRingOff64; u++) ring[u] = fetch(u);
+    for (uint32_t k = 0; k < K; k += kRingOff64) {
 #pragma unroll
-        for (int u = 0; u < kRingOff; u++) {
+        for (int u = 0; u < kRingOff64; u++) {
             const uint4 v = ring[u];
             const uint32_t kk = k + u;
-            ring[u] = fetch(kk + kRingOff);
+            ring[u] = fetch(kk + kRingOff64);
             if (kk < K) {
                 uint64_t w0 = lo64(v), w1 = hi64(v);
                 if (kk < kc0 || kk >= kc1) {

@@ -175,11 +175,11 @@ KLaunch pick_fixed(int log2g, bool aligned, bool nt, bool light) {
 
 // Non-temporal payload loads when the batch is far larger than the 256 MiB
 // Infinity Cache (MCHECKSUM_GPU_NT=0/1 overrides).
-// Small batches take the light CRC-32C layout (16 KiB LDS fill, 256-thread
+// Small batches (<= 16 MiB) take the light CRC-32C layout (16 KiB LDS fill, 256-thread
 // workgroups over every CU, 64 lanes per payload): the full layout's 140 KiB
 // fill and 1024-thread workgroups cost ~6-12 us per call there
 // (profiles/r01/latency.json).  MCHECKSUM_GPU_LIGHT=0/1 overrides.
-constexpr uint64_t kLightMaxBytes = 8ull << 20;
+constexpr uint64_t kLightMaxBytes = 16ull << 20;  // crossover ~24 MiB (latency.json)
 bool use_light(uint64_t batch_bytes, bool known) {
     const char *env = getenv("MCHECKSUM_GPU_LIGHT");
     if (env && env[0]) return env[0] == '1';

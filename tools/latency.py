@@ -17,7 +17,7 @@ def main():
     G.fill_splitmix(big, 1)
     for light in ("0", "1"):
       os.environ["MCHECKSUM_GPU_LIGHT"] = light
-      for count in (1, 8, 64, 256, 1024, 4096):
+      for count in (1, 8, 64, 256, 1024, 4096, 8192, 16384):
           out = torch.empty(count, dtype=torch.int32, device="cuda")
           f = lambda: G.checksum_fixed("crc32c", big, length, count=count, out=out)
           for _ in range(5):
