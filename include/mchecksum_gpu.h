@@ -147,6 +147,14 @@ mchecksum_gpu_lanes_per_payload(const char *hash_method, size_t len);
 MCHECKSUM_PUBLIC const char *
 mchecksum_gpu_last_error(void);
 
+/* Diagnostics: the number of work-queue protocol faults the batch kernels
+ * counted on the current device since the library was loaded (0 in a
+ * healthy run; every wait inside a launch is bounded, and a wait that gives
+ * up is counted here instead of hanging the GPU).  Synchronizes the device.
+ * Returns -1 without a usable device. */
+MCHECKSUM_PUBLIC long long
+mchecksum_gpu_queue_faults(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -58,9 +58,10 @@ struct Tab32 {
 // high-nibble tables are NOT replicated: entry v sits at v*16 B, so the masked
 // byte (v << 4) is its own address and the 16 entries fall on 16 distinct bank
 // pairs of ds_read_b64 (lanes that share an entry broadcast) -- conflict-free
-// without copies.  Then the combine operators (nibble tables, 2 KiB each).
+// without copies.  Tables p and p+4 share a 256-B block (p+4 at +8 B).  Then
+// the combine operators (nibble tables, 2 KiB each).
 constexpr uint32_t kL64Hi = 32768;
-constexpr uint32_t kL64Main = kL64Hi + 8 * 256;
+constexpr uint32_t kL64Main = kL64Hi + 4 * 256;
 constexpr uint32_t kL64Bytes = kL64Main + CRC64_NOPS_MAX * 2048;
 // CRC-64 is VALU-bound (the table XOR tree); two 1024-thread workgroups per CU
 // (8 waves/SIMD, 80 KiB LDS each) hide the LDS latency.  MCK_CRC64_SPLIT=1
@@ -115,7 +116,270 @@ struct BatchArgs {
     // message mode (verify_messages): payload i = [offsets[i] + pay_off,
     // offsets[i+1]), expected CRC = big-endian u32 at offsets[i] + hash_off
     uint32_t msg, pay_off, hash_off;
+    // work-queue slot (WorkQueue below); nullptr = static assignment
+    unsigned long long *queue;
 };
+
+// ------------------------------------------------------------ work queue --
+// Dynamic distribution of payloads over waves.  With a static assignment the
+// waves of one 4 GiB launch finish between 566 and 642 us (p10..max; the XCDs
+// stream at different rates, profiles/r01/tail_trace.json), so the slowest
+// wave sets the launch time.  Per-wave tickets from global counters do not
+// work: device-scope atomics on one address retire ~1 per 45 ns on MI355X,
+// so 8 per-XCD counters fed one ticket per payload group throttled C2 2.6x.
+//
+// Two levels instead.  Units [0, n) form chunks of 2^cl units; the chunk
+// ids are dealt round-robin to 8 sub-queues (one per XCD by blockIdx % 8, the
+// dispatch order), each a global counter on its own 256-B line.  A
+// workgroup takes whole chunks (one global atomic per 16 units, stealing from
+// the next sub-queue once its own is drained) and its waves take the chunk's
+// units one at a time through an LDS counter.  The wave that takes a chunk's
+// first slot fetches the NEXT chunk, so a fetch's latency hides under a whole
+// chunk of scanning; chunk ids pass through a small LDS ring whose entries
+// are recycled only after all 2^cl readers of the previous occupant have
+// read it.  The last wave of the grid zeroes the global counters, leaving the
+// slot ready for the next launch (the host hands each launch a slot from a
+// ring, mchecksum_gpu.hip).
+// Slot layout (one counter per 256-B line): [0, 8) sub-queue tickets,
+// [8, 16) exited workgroups per group (blockIdx % 8), [16] exited groups.
+constexpr uint32_t kQSub = 8;
+constexpr uint32_t kQStride = 32;  // u64 words between counters
+constexpr uint32_t kQGroupDone = kQSub;
+constexpr uint32_t kQAllDone = 2 * kQSub;
+constexpr uint32_t kQSlotWords = (2 * kQSub + 1) * kQStride;
+// Chunk size: a power of two, about a quarter of a workgroup's fair share
+// of units, between 1 and 32 (C4: 32 units; a 5000-payload batch: 4).
+// Fixed 16 starved half the workgroups of C3's 8192 units at 2 WGs per CU; 32
+// beat 16 on the large batches.  The next chunk is fetched when a quarter of
+// the current one is left to take: early enough to hide the fetch (~1.3 us
+// mean), late enough that a workgroup holds little unstarted work when the
+// queue runs dry.
+constexpr uint32_t kWgChunkMaxLog2 = 5;
+// Which batches take the queue (profiles/r01/ab12_work_queue.log, medians
+// vs the static split): variable-length (offsets) batches, +4% C4 and +8%
+// C4-layout CRC-64 over the byte-balanced static split, and the large
+// (non-temporal, >= 512 MiB) aligned CRC-32C batches, +2.3% on the headline.
+// Smaller fixed batches and CRC-64 fixed batches keep the static stride:
+// there the queue's fixed costs outweigh the balance (C2 -11%, C3 -5%).
+// MCK_DYN_FIXED=1 builds every throughput kernel with the queue (A/B).
+#ifndef MCK_DYN_FIXED
+#define MCK_DYN_FIXED 0
+#endif
+__host__ __device__ constexpr bool dyn_policy(int width, int mode, bool nt, bool light) {
+    return !light && (mode == 2 || (width == 32 && nt && mode == 0) || MCK_DYN_FIXED);  // 2 = kOffsets
+}
+__device__ __forceinline__ uint32_t chunk_log2(uint64_t n) {
+    const uint64_t share = n / (4ull * gridDim.x);
+    uint32_t l = 0;
+    while (l < kWgChunkMaxLog2 && (2ull << l) <= share) l++;
+    return l;
+}
+constexpr uint32_t kWgRing = 8;    // LDS ring of published chunk ids
+constexpr uint64_t kNoChunk = 0xFFFFFFFFull;
+
+struct WgQueue {
+    unsigned int slot;     // next (chunk, unit) slot of this workgroup
+    unsigned int drained;  // sub-queues (counted from home) found empty
+    unsigned int exited;   // waves of this workgroup that left the loop
+    unsigned int reads[kWgRing];
+    unsigned long long entry[kWgRing];  // (chunk seq << 32) | global chunk id
+};
+
+__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
+    return (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32 |
+           __builtin_amdgcn_readfirstlane((uint32_t)v);
+}
+
+template <class T>
+__device__ __forceinline__ T lds_ld(T *p) {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+template <class T>
+__device__ __forceinline__ void lds_st(T *p, T v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Every wait in the queue protocol is bounded: a wait that exceeds ~1 s (or a
+// wave that takes more slots than the launch has) counts a fault in
+// g_mck_queue_faults (read by mchecksum_gpu_queue_faults()) and
+// leaves the loop, so a protocol failure shows up as a fault count and wrong
+// values in tests instead of a wedged GPU.  Diagnostic builds (-DMCK_TRACE=1)
+// also record where (g_mck_qdiag).
+__device__ unsigned int g_mck_queue_faults;
+#if MCK_TRACE
+__device__ unsigned long long g_mck_qdiag[4 * 64];
+__device__ unsigned int g_mck_qdiag_n;
+// per wave: fetches, fetch ticks (sum), fetch ticks (max), entry-wait ticks
+__device__ unsigned long long g_mck_qwave[6 * 16384];
+#endif
+__device__ __noinline__ void queue_fault(uint32_t kind, uint64_t a, uint64_t b) {
+    atomicAdd(&g_mck_queue_faults, 1u);
+#if MCK_TRACE
+    const unsigned int i = atomicAdd(&g_mck_qdiag_n, 1u);
+    if (i < 64) {
+        g_mck_qdiag[4 * i] = kind;
+        g_mck_qdiag[4 * i + 1] = blockIdx.x * 64ull + (threadIdx.x >> 6);
+        g_mck_qdiag[4 * i + 2] = a;
+        g_mck_qdiag[4 * i + 3] = b;
+    }
+#else
+    (void)kind;
+    (void)a;
+    (void)b;
+#endif
+}
+constexpr uint32_t kSpinMax = 1u << 24;
+#define MCK_SPIN_GUARD(cnt, kind, A_, B_) \
+    if (++(cnt) > kSpinMax) {             \
+        queue_fault(kind, A_, B_);        \
+        break;                            \
+    }
+
+// One lane: the next global chunk id for this workgroup, or kNoChunk.
+__device__ uint64_t wg_fetch(WgQueue *L, unsigned long long *q, uint64_t nch) {
+    const uint32_t home = blockIdx.x % kQSub;
+    uint32_t d = lds_ld(&L->drained);
+    while (d < kQSub) {
+        const uint32_t k = (home + d) % kQSub;
+        // sub-queue k owns chunks k, k + 8, k + 16, ...: every XCD streams
+        // from the same moving window of the batch (contiguous per-XCD ranges
+        // -- 8 windows far apart -- measured 8% slower on the headline batch)
+        const uint64_t t = atomicAdd(q + k * kQStride, 1ull);
+        if (k + t * kQSub < nch) return k + t * kQSub;
+        atomicMax(&L->drained, d + 1);
+        const uint32_t seen = lds_ld(&L->drained);
+        d = seen > d + 1 ? seen : d + 1;
+    }
+    return kNoChunk;
+}
+
+// One lane: make chunk `seq` of this workgroup known in the ring.
+__device__ void wg_publish(WgQueue *L, uint32_t seq, uint64_t id, uint32_t cl) {
+    const uint32_t r = seq % kWgRing;
+    uint32_t spins = 0;
+    (void)spins;
+    if (seq >= kWgRing)
+        while (lds_ld(&L->reads[r]) != (1u << cl)) {
+            __builtin_amdgcn_s_sleep(1);
+            MCK_SPIN_GUARD(spins, 1, seq, lds_ld(&L->reads[r]))
+        }
+    lds_st(&L->reads[r], 0u);
+    lds_st(&L->entry[r], (unsigned long long)seq << 32 | id);
+}
+
+// Thread 0, before the kernel's first barrier: reset the LDS state and
+// publish the first chunk (its fetch overlaps the LDS table fill).
+__device__ void wg_queue_init(WgQueue *L, unsigned long long *q, uint64_t n) {
+    L->slot = 0;
+    L->drained = 0;
+    L->exited = 0;
+    for (uint32_t r = 0; r < kWgRing; r++) {
+        L->reads[r] = 0;
+        L->entry[r] = ~0ull;
+    }
+    const uint32_t cl = chunk_log2(n);
+    wg_publish(L, 0, wg_fetch(L, q, (n + (1ull << cl) - 1) >> cl), cl);
+}
+
+// Calls body(u) for this wave's units: through the work queue (DYN: the
+// throughput kernels; the host always passes a slot, wg_queue_init has run)
+// or u = wave, wave + nw, ... (the light layout's small batches).  One path
+// per kernel: both in one kernel cost the register-tight CRC-64 loops spills.
+template <bool DYN, class F>
+__device__ __forceinline__ void for_each_unit(WgQueue *L, unsigned long long *queue, uint64_t n, uint32_t wave,
+                                              uint32_t nw, F &&body) {
+    if constexpr (DYN) {
+        const bool l0 = (threadIdx.x & 63u) == 0;
+        const uint32_t cl = chunk_log2(n), cu = 1u << cl, lead = cu > 4 ? cu / 4 : 1;
+        const uint64_t nch = (n + cu - 1) >> cl;
+#if MCK_TRACE
+        unsigned long long qs_n = 0, qs_sum = 0, qs_max = 0, qs_wait = 0, qs_busy = 0, qs_units = 0;
+#endif
+        const uint64_t max_iters = (uint64_t)cu * nch + 4ull * cu + 64;
+        uint64_t iters = 0;
+        for (;;) {
+            uint64_t e = 0;
+            uint32_t t = 0;
+            if (++iters > max_iters) {  // more slots than the launch has: protocol fault
+                if (l0) queue_fault(3, iters, 0);
+                break;
+            }
+            if (l0) {
+                t = atomicAdd(&L->slot, 1u);
+                const uint32_t seq = t >> cl, r = seq % kWgRing;
+                uint32_t spins = 0;
+                (void)spins;
+#if MCK_TRACE
+                const unsigned long long w0 = wall_clock64();
+                unsigned long long f0 = 0;
+#endif
+                while (((e = lds_ld(&L->entry[r])) >> 32) != seq) {
+                    __builtin_amdgcn_s_sleep(1);
+                    MCK_SPIN_GUARD(spins, 2, seq, e)
+                }
+#if MCK_TRACE
+                qs_wait += wall_clock64() - w0;
+#endif
+                if ((e >> 32) != seq) e = kNoChunk;  // gave up (fault counted)
+                atomicAdd(&L->reads[r], 1u);
+                // One taker per chunk (slot cu - lead) fetches the next
+                // chunk -- after its own chunk is known, so fetches run in chunk
+                // order and the first kNoChunk is final.
+                if ((t & (cu - 1)) == cu - lead) {
+#if MCK_TRACE
+                    f0 = wall_clock64();
+#endif
+                    const uint64_t nid = (e & 0xFFFFFFFFull) == kNoChunk ? kNoChunk : wg_fetch(L, queue, nch);
+#if MCK_TRACE
+                    const unsigned long long df = wall_clock64() - f0;
+                    qs_n++;
+                    qs_sum += df;
+                    qs_max = df > qs_max ? df : qs_max;
+#endif
+                    wg_publish(L, seq + 1, nid, cl);
+                }
+            }
+            t = __builtin_amdgcn_readfirstlane(t);
+            const uint64_t id = uniform64(e) & 0xFFFFFFFFull;
+            if (id == kNoChunk) break;
+            const uint64_t u = (id << cl) + (t & (cu - 1));
+#if MCK_TRACE
+            const unsigned long long b0 = wall_clock64();
+#endif
+            if (u < n) body(u);
+#if MCK_TRACE
+            qs_busy += wall_clock64() - b0;
+            qs_units += u < n;
+#endif
+        }
+#if MCK_TRACE
+        if (l0 && wave < 16384u) {
+            g_mck_qwave[4 * wave] = qs_n;
+            g_mck_qwave[4 * wave + 1] = qs_sum;
+            g_mck_qwave[4 * wave + 2] = qs_max;
+            g_mck_qwave[4 * wave + 3] = qs_wait;
+            g_mck_qwave[4 * 16384 + 2 * wave] = qs_units;
+            g_mck_qwave[4 * 16384 + 2 * wave + 1] = qs_busy;
+        }
+#endif
+        // Exit counting is hierarchical: one global atomic per wave on a
+        // single line serialised ~4096 x 45 ns at the end of every launch
+        // (C2 ran 2x slower).  Waves count in LDS, the last wave of a
+        // workgroup counts in its group's line, the last workgroup of a group
+        // in the slot's line; the last group zeroes the slot.
+        if (l0 && atomicAdd(&L->exited, 1u) == blockDim.x / 64u - 1u) {
+            const uint32_t g = blockIdx.x % kQSub;
+            const uint32_t wgs = (gridDim.x - g + kQSub - 1) / kQSub;  // workgroups in group g
+            const uint32_t groups = gridDim.x < kQSub ? gridDim.x : kQSub;
+            if (atomicAdd(queue + (kQGroupDone + g) * kQStride, 1ull) == wgs - 1ull &&
+                atomicAdd(queue + kQAllDone * kQStride, 1ull) == groups - 1ull)
+                for (uint32_t j = 0; j <= kQAllDone; j++) atomicExch(queue + j * kQStride, 0ull);
+        }
+        (void)nw;
+    } else {
+        for (uint64_t u = wave; u < n; u += nw) body(u);
+    }
+}
 
 // Network-order u32 at an arbitrary byte address (the HG header's payload
 // hash, src/mercury_header.c:111-112 writes it with htonl).
@@ -413,6 +677,20 @@ __device__ __forceinline__ void wave_range(const uint64_t *off, uint64_t count, 
     *last = wave + 1 == nw ? count : lower_bound_u64(off, count, hi);
 }
 
+// Diagnostic build (-DMCK_TRACE=1, tools/tail_trace.py): per-wave clock
+// stamps (kernel entry, after the LDS fill, exit) of the last launch.
+#ifndef MCK_TRACE
+#define MCK_TRACE 0
+#endif
+#if MCK_TRACE
+constexpr int kTraceWaves = 16384;
+__device__ unsigned long long g_mck_trace[3 * kTraceWaves];
+#define MCK_STAMP(w, k) \
+    do { if ((threadIdx.x & 63u) == 0 && (w) < kTraceWaves) g_mck_trace[3 * (w) + (k)] = wall_clock64(); } while (0)
+#else
+#define MCK_STAMP(w, k) do { } while (0)
+#endif
+
 template <typename T, bool VERIFY>
 __device__ __forceinline__ void emit(const BatchArgs &a, uint64_t p, T v) {
     if (VERIFY) {
@@ -432,11 +710,17 @@ __global__ __launch_bounds__(kBlk32<LIGHT>, 1) void crc32c_batch_kernel(BatchArg
     constexpr int kWavesPerBlock = kBlk32<LIGHT> / 64;
     __shared__ __attribute__((aligned(16))) uint8_t lds_raw[LIGHT ? kL32LightBytes : kL32Bytes];
     const crc32_gpu_pack_t *pk = reinterpret_cast<const crc32_gpu_pack_t *>(a.pack);
+    MCK_STAMP(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6), 0);
+    constexpr int PPW = 64 >> LOG2G;
+    const uint64_t units = MODE == kOffsets ? a.count : (a.count + PPW - 1) / PPW;
+    __shared__ WgQueue wgq;
+    constexpr bool DYN = dyn_policy(32, MODE, NT, LIGHT);
+    if (DYN && threadIdx.x == 0) wg_queue_init(&wgq, a.queue, units);
     fill_lds32<LIGHT, kBlk32<LIGHT>>(lds_raw, pk);
     __syncthreads();
+    MCK_STAMP(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6), 1);
     const Tab32<LIGHT> lds{lds_raw};
 
-    constexpr int PPW = 64 >> LOG2G;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t gl = lane & ((1u << LOG2G) - 1u), grp = lane >> LOG2G;
     const uint32_t lc0 = (lane & 31u) << 2, lc1 = lc0 | 0x10000u;
@@ -445,9 +729,7 @@ __global__ __launch_bounds__(kBlk32<LIGHT>, 1) void crc32c_batch_kernel(BatchArg
     const uint32_t nw = gridDim.x * kWavesPerBlock;
 
     if (MODE == kOffsets) {
-        uint64_t first, last;
-        wave_range(a.offsets, a.count, wave, nw, &first, &last);
-        for (uint64_t p = first; p < last; p++) {
+        auto one = [&](uint64_t p) {
             const uint64_t m0 = a.offsets[p], m1 = a.offsets[p + 1];
             // message mode: a message shorter than its headers fails verification
             const bool short_msg = a.msg && m1 - m0 < a.pay_off;
@@ -464,11 +746,19 @@ __global__ __launch_bounds__(kBlk32<LIGHT>, 1) void crc32c_batch_kernel(BatchArg
                     emit<uint32_t, VERIFY>(a, p, x ^ xorout);
                 }
             }
+        };
+        if constexpr (!LIGHT) {
+            for_each_unit<true>(&wgq, a.queue, units, wave, nw, one);
+        } else {  // static: a byte-balanced contiguous range per wave
+            uint64_t first, last;
+            wave_range(a.offsets, a.count, wave, nw, &first, &last);
+            for (uint64_t p = first; p < last; p++) one(p);
         }
+        MCK_STAMP(wave, 2);
         return;
     }
-    for (uint64_t pb = (uint64_t)wave * PPW; pb < a.count; pb += (uint64_t)nw * PPW) {
-        const uint64_t p = pb + grp;
+    for_each_unit<DYN>(&wgq, a.queue, units, wave, nw, [&](uint64_t u) {
+        const uint64_t p = u * PPW + grp;
         const bool act = p < a.count;
         const uint64_t pc = act ? p : a.count - 1;
         uint32_t x;
@@ -477,7 +767,8 @@ __global__ __launch_bounds__(kBlk32<LIGHT>, 1) void crc32c_batch_kernel(BatchArg
         else
             x = payload32_generic<LOG2G, NT>(lds, pk, a.base + pc * a.stride, a.len, gl, lc0, lc1);
         if (act && gl == 0) emit<uint32_t, VERIFY>(a, p, x ^ xorout);
-    }
+    });
+    MCK_STAMP(wave, 2);
 }
 
 // ----------------------------------------------------------------- CRC-64 --
@@ -550,7 +841,7 @@ __device__ __forceinline__ void f64x_byte(const uint8_t *lds, uint32_t xl, uint3
     r[4 * B + 1] = lds64(lds, sdwa_hi<B>(xl) + kL64Hi + B * 256);
     sdwa_lo<B>(ln.al[B], xh);
     r[4 * B + 2] = lds64(lds, ln.al[B] + (B + 4) * 4096);
-    r[4 * B + 3] = lds64(lds, sdwa_hi<B>(xh) + kL64Hi + (B + 4) * 256);
+    r[4 * B + 3] = lds64(lds, sdwa_hi<B>(xh) + kL64Hi + B * 256 + 8);
 #else
     const uint32_t sl = 0x0C0C0400u | ((uint32_t)B << 8);  // byte B -> address byte 1, lane byte -> 0
     const uint32_t sh = 0x0C0C0C04u | (uint32_t)B;         // byte B -> address byte 0
@@ -559,7 +850,7 @@ __device__ __forceinline__ void f64x_byte(const uint8_t *lds, uint32_t xl, uint3
     r[4 * B + 0] = lds64(lds, __builtin_amdgcn_perm(l0, ln.lc, sl) + B * 4096);
     r[4 * B + 1] = lds64(lds, __builtin_amdgcn_perm(h0, h0, sh) + kL64Hi + B * 256);
     r[4 * B + 2] = lds64(lds, __builtin_amdgcn_perm(l1, ln.lc, sl) + (B + 4) * 4096);
-    r[4 * B + 3] = lds64(lds, __builtin_amdgcn_perm(h1, h1, sh) + kL64Hi + (B + 4) * 256);
+    r[4 * B + 3] = lds64(lds, __builtin_amdgcn_perm(h1, h1, sh) + kL64Hi + B * 256 + 8);
 #endif
 }
 
@@ -615,7 +906,10 @@ __device__ void fill_lds64(uint8_t *lds, const crc64_gpu_pack_t *pk) {
         const uint64_t v = pk->main[2 * (d >> 9)][(d >> 5) & 15u];
         l4[q] = make_uint4((uint32_t)v, (uint32_t)(v >> 32), (uint32_t)v, (uint32_t)(v >> 32));
     }
-    for (uint32_t d = threadIdx.x; d < 128u; d += BLOCK) l[kL64Hi / 8 + (d >> 4) * 32 + (d & 15u) * 2] = pk->main[2 * (d >> 4) + 1][d & 15u];
+    for (uint32_t d = threadIdx.x; d < 128u; d += BLOCK) {
+        const uint32_t p = d >> 4, v = d & 15u;  // table p, entry v
+        l[kL64Hi / 8 + (p & 3u) * 32 + (p >> 2) + v * 2] = pk->main[2 * p + 1][v];
+    }
     if constexpr (!OG) {
         const uint4 *ops = reinterpret_cast<const uint4 *>(&pk->ops[0][0][0]);
         const uint32_t nops = pk->nops * 128u;
@@ -797,10 +1091,14 @@ __global__ __launch_bounds__(kBlk64<MODE>, kWpe64<MODE>) void crc64_batch_kernel
     constexpr int kWPB = S::block / 64;
     __shared__ __attribute__((aligned(16))) uint8_t lds[S::lds64_bytes];
     const crc64_gpu_pack_t *pk = reinterpret_cast<const crc64_gpu_pack_t *>(a.pack);
+    constexpr int PPW = 64 >> LOG2G;
+    const uint64_t units = MODE == kOffsets ? a.count : (a.count + PPW - 1) / PPW;
+    __shared__ WgQueue wgq;
+    constexpr bool DYN = dyn_policy(64, MODE, NT, false);
+    if (DYN && threadIdx.x == 0) wg_queue_init(&wgq, a.queue, units);
     fill_lds64<S::block, S::ops_global>(lds, pk);
     __syncthreads();
 
-    constexpr int PPW = 64 >> LOG2G;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t gl = lane & ((1u << LOG2G) - 1u), grp = lane >> LOG2G;
     const uint32_t lc = (lane & 31u) << 3;
@@ -809,19 +1107,18 @@ __global__ __launch_bounds__(kBlk64<MODE>, kWpe64<MODE>) void crc64_batch_kernel
     const uint32_t nw = gridDim.x * kWPB;
 
     if (MODE == kOffsets) {
-        uint64_t first, last;
-        wave_range(a.offsets, a.count, wave, nw, &first, &last);
-        for (uint64_t p = first; p < last; p++) {
+        auto one = [&](uint64_t p) {
             const uint64_t o = a.offsets[p];
             const uint64_t n = a.offsets[p + 1] - o;
             const uint64_t x = n < (1ull << 31) ? payload64_g64<NT>(lds, pk, a.base + o, n, gl, lc)
                                                 : payload64_generic<LOG2G, NT>(lds, pk, a.base + o, n, gl, lc);
             if (gl == 0) emit<uint64_t, VERIFY>(a, p, x ^ xorout);
-        }
+        };
+        for_each_unit<true>(&wgq, a.queue, units, wave, nw, one);
         return;
     }
-    for (uint64_t pb = (uint64_t)wave * PPW; pb < a.count; pb += (uint64_t)nw * PPW) {
-        const uint64_t p = pb + grp;
+    for_each_unit<DYN>(&wgq, a.queue, units, wave, nw, [&](uint64_t u) {
+        const uint64_t p = u * PPW + grp;
         const bool act = p < a.count;
         const uint64_t pc = act ? p : a.count - 1;
         uint64_t x;
@@ -830,7 +1127,7 @@ __global__ __launch_bounds__(kBlk64<MODE>, kWpe64<MODE>) void crc64_batch_kernel
         else
             x = payload64_generic<LOG2G, NT>(lds, pk, a.base + pc * a.stride, a.len, gl, lc);
         if (act && gl == 0) emit<uint64_t, VERIFY>(a, p, x ^ xorout);
-    }
+    });
 }
 
 }  // namespace

@@ -21,7 +21,15 @@ struct DevCtx {
     int cus = 0;
     void *pack[MCK_NMODELS][CRC_GPU_MAX_LOG2G + 1] = {};
     void *ext[MCK_NMODELS] = {};  // mchecksum_gpu_ext.hip's per-model tables
+    // Work-queue slots of the batch kernels (WorkQueue, crc_gpu_device.h): a
+    // ring of kQueueSlots zeroed counter sets; each launch takes the next slot
+    // and its last wave re-zeroes it.  Launches that run at the same time
+    // (different streams) get different slots unless more than kQueueSlots
+    // are in flight at once.
+    unsigned long long *queue = nullptr;
+    uint32_t queue_next = 0;
 };
+constexpr uint32_t kQueueSlots = 4096;
 
 extern std::mutex g_mu;
 
@@ -34,6 +42,8 @@ int gpu_model(const char *method, int *width);
 int device_ctx(DevCtx **out);
 // Model + device context + table pack for lanes-per-payload 2^log2g (takes g_mu).
 int prologue(const char *method, int log2g, int *width, DevCtx **c, const void **pack);
+// Work-queue slot for one launch of a throughput (non-light) batch kernel.
+unsigned long long *queue_slot(DevCtx *c);
 
 }  // namespace mck
 

@@ -75,6 +75,14 @@ int device_ctx(DevCtx **out) {
         e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         if (e != hipSuccess) return hip_err(e, "hipDeviceGetAttribute");
         c.cus = cus > 0 ? cus : 1;
+        const size_t qbytes = (size_t)kQueueSlots * kQSlotWords * sizeof(unsigned long long);
+        e = hipMalloc(reinterpret_cast<void **>(&c.queue), qbytes);
+        if (e == hipSuccess) e = hipMemset(c.queue, 0, qbytes);
+        if (e != hipSuccess) {
+            if (c.queue) (void)hipFree(c.queue);
+            c.queue = nullptr;
+            return hip_err(e, "work-queue allocation");
+        }
         c.init = true;
     }
     *out = &c;
@@ -120,6 +128,11 @@ int get_pack(DevCtx *c, int idx, int log2g, const void **pack) {
     c->pack[idx][log2g] = d;
     *pack = d;
     return 0;
+}
+
+unsigned long long *queue_slot(DevCtx *c) {
+    const uint32_t s = __atomic_fetch_add(&c->queue_next, 1u, __ATOMIC_RELAXED) % kQueueSlots;
+    return c->queue + (size_t)s * kQSlotWords;
 }
 
 typedef void (*kern_t)(BatchArgs);
@@ -228,6 +241,9 @@ int prologue(const char *method, int log2g, int *width, DevCtx **c, const void *
     return get_pack(*c, idx, log2g, pack);
 }
 
+// The work queue's chunk ids are 32-bit (crc_gpu_device.h, WgQueue).
+constexpr uint64_t kMaxUnits = kNoChunk - 1;  // chunk ids < 2^32 even at one unit per chunk
+
 int do_offsets(const char *method, const void *base, const uint64_t *offsets, size_t count, void *out,
                const void *expected, uint8_t *status, uint32_t *mism, void *stream, bool verify,
                bool msg = false, size_t pay_off = 0, size_t hash_off = 0) {
@@ -235,6 +251,7 @@ int do_offsets(const char *method, const void *base, const uint64_t *offsets, si
         return set_err(MCHECKSUM_GPU_EINVAL, "NULL pointer argument%s%d");
     if (msg && (hash_off + 4 > pay_off || pay_off > (1u << 30)))
         return set_err(MCHECKSUM_GPU_EINVAL, "hash_offset + 4 must not exceed payload_offset%s%d");
+    if ((uint64_t)count > kMaxUnits) return set_err(MCHECKSUM_GPU_EINVAL, "more than 2^32 - 2 payloads in one call%s%d");
     if (!mchecksum_gpu_available()) return set_err(MCHECKSUM_GPU_ENODEV, "no HIP device%s%d");
     int width = 0;
     DevCtx *c = nullptr;
@@ -254,6 +271,7 @@ int do_offsets(const char *method, const void *base, const uint64_t *offsets, si
     a.msg = msg ? 1u : 0u;
     a.pay_off = (uint32_t)pay_off;
     a.hash_off = (uint32_t)hash_off;
+    a.queue = nullptr;
     if (msg && width != 32)
         return set_err(MCHECKSUM_GPU_EMETHOD, "message verify carries a 32-bit header hash: crc32c only%s%d");
     KLaunch k;
@@ -271,6 +289,7 @@ int do_offsets(const char *method, const void *base, const uint64_t *offsets, si
     else
         k = verify ? (nt ? kernel_ptr<64, 6, kOffsets, true, true>() : kernel_ptr<64, 6, kOffsets, true>())
                    : (nt ? kernel_ptr<64, 6, kOffsets, false, true>() : kernel_ptr<64, 6, kOffsets, false>());
+    if (dyn_policy(width, kOffsets, nt, light)) a.queue = queue_slot(c);
     return launch(k, a, grid_for(c, count, k), stream);
 }
 
@@ -291,6 +310,7 @@ int launch_fixed(DevCtx *c, const void *pack, int width, int lg, const void *dev
     const bool nt = !light && use_nt((uint64_t)len * count);
     const KLaunch k = width == 32 ? pick_fixed<32>(lg, aligned, nt, light) : pick_fixed<64>(lg, aligned, nt, false);
     const uint64_t ppw = 64u >> lg;
+    a.queue = dyn_policy(width, aligned ? kFixedAligned : kFixedGeneric, nt, light) ? queue_slot(c) : nullptr;
     return launch(k, a, grid_for(c, (count + ppw - 1) / ppw, k), stream);
 }
 
@@ -331,6 +351,7 @@ int mchecksum_gpu_checksum_fixed(const char *hash_method, const void *dev_base, 
                                  size_t count, void *dev_out, void *stream) {
     if (count && (!dev_base || !dev_out)) return set_err(MCHECKSUM_GPU_EINVAL, "NULL pointer argument%s%d");
     if (count > 1 && stride < len) return set_err(MCHECKSUM_GPU_EINVAL, "stride smaller than len%s%d");
+    if ((uint64_t)count > kMaxUnits) return set_err(MCHECKSUM_GPU_EINVAL, "more than 2^32 - 2 payloads in one call%s%d");
     if (!mchecksum_gpu_available()) return set_err(MCHECKSUM_GPU_ENODEV, "no HIP device%s%d");
     int width = 0;
     if (gpu_model(hash_method, &width) >= 0 && width == 32 && use_light((uint64_t)len * count, true)) {
@@ -371,5 +392,32 @@ int mchecksum_gpu_verify_messages(const char *hash_method, const void *dev_buf, 
 }
 
 const char *mchecksum_gpu_last_error(void) { return t_err; }
+
+long long mchecksum_gpu_queue_faults(void) {
+    if (!mchecksum_gpu_available()) return -1;
+    unsigned int n = 0;
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_mck_queue_faults), sizeof(n), 0, hipMemcpyDeviceToHost) != hipSuccess)
+        return -1;
+    return n;
+}
+
+#if MCK_TRACE
+// Diagnostic builds only: copy the per-wave stamps of the last launch.
+MCHECKSUM_PUBLIC int mck_debug_trace_read(void *host, size_t bytes) {
+    if (bytes > sizeof(g_mck_trace)) bytes = sizeof(g_mck_trace);
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_mck_trace), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+// ... the per-wave work-queue timings of the last launch ...
+MCHECKSUM_PUBLIC int mck_debug_qwave_read(void *host, size_t bytes) {
+    if (bytes > sizeof(g_mck_qwave)) bytes = sizeof(g_mck_qwave);
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_mck_qwave), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+// ... and the work-queue fault records (count, then 4 words per record).
+MCHECKSUM_PUBLIC int mck_debug_qdiag_read(unsigned int *n, unsigned long long *rec) {
+    if (hipMemcpyFromSymbol(n, HIP_SYMBOL(g_mck_qdiag_n), sizeof(*n), 0, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    return hipMemcpyFromSymbol(rec, HIP_SYMBOL(g_mck_qdiag), sizeof(g_mck_qdiag), 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
 
 }  // extern "C"

@@ -53,6 +53,13 @@ def gpu_available() -> bool:
     return bool(_lib().mchecksum_gpu_available())
 
 
+def queue_faults() -> int:
+    """Work-queue protocol faults the batch kernels counted on the current
+    device since load (bounded waits that gave up; 0 when healthy).
+    Synchronizes the device."""
+    return int(_lib().mchecksum_gpu_queue_faults())
+
+
 def prepare(method: str = "crc32c") -> None:
     rc = _lib().mchecksum_gpu_prepare(method.encode())
     if rc != 0:

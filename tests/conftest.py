@@ -40,3 +40,18 @@ def gpu():
     from mercury_amd import gpu as G
     assert G.gpu_available(), "libmchecksum sees no HIP device"
     return G
+
+
+@pytest.fixture(autouse=True)
+def _no_queue_faults(request):
+    """Every GPU test also checks that the batch kernels' work queue never gave
+    up a wait (crc_gpu_device.h: bounded waits count a fault instead of
+    hanging)."""
+    yield
+    if request.node.get_closest_marker("gpu") is None:
+        return
+    import torch
+    if not torch.cuda.is_available():
+        return
+    from mercury_amd import gpu as G
+    assert G.queue_faults() == 0, "work-queue protocol fault counted (mchecksum_gpu_queue_faults)"

@@ -1,0 +1,79 @@
+"""Stress the batch kernels' dynamic work queue: many launches of random
+shapes (fixed and offsets batches, both methods, every lanes-per-payload
+width, both load policies) on the throughput layout, each checked bit for bit against the CPU
+oracle, with a host watchdog (a launch not done after 20 s ends the process
+with exit 3 instead of waiting on a wedged GPU).  Ends with the device's
+queue fault count (must be 0)."""
+import os
+import time
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _wait(torch, tag):
+    ev = torch.cuda.Event()
+    ev.record()
+    t0 = time.time()
+    while not ev.query():
+        if time.time() - t0 > 20:
+            print("HUNG", tag, flush=True)
+            os._exit(3)
+        time.sleep(0.002)
+
+
+@pytest.mark.parametrize("n_iter", [240])
+def test_dynamic_queue_random_shapes(gpu, oracle_mod, n_iter, monkeypatch):
+    import torch
+    G, O = gpu, oracle_mod
+    rng = np.random.default_rng(12345)
+    monkeypatch.setenv("MCHECKSUM_GPU_LIGHT", "0")
+    host = O.splitmix_bytes(64 << 20, 99)
+    dev = torch.from_numpy(host).cuda()
+    dev = torch.cat([dev, torch.zeros(64, dtype=torch.uint8, device="cuda")])
+    bad = 0
+    t0 = time.time()
+    for it in range(n_iter):
+        method = ("crc32c", "crc64")[it % 2]
+        if rng.random() < 0.5:
+            length = int(rng.choice([0, 1, 16, 1000, 4096, 4100, 16384, 65536, 100003]))
+            stride = length + int(rng.choice([0, 0, 16, 3]))
+            maxc = max(1, (64 << 20) // max(stride, 1) - 1)
+            count = int(min(maxc, rng.choice([1, 2, 15, 16, 17, 67, 255, 256, 1000, 4097, 20000])))
+            if length == 0:
+                stride = 16
+            lg = rng.choice([None, 0, 2, 4, 6])
+            if lg is None:
+                monkeypatch.delenv("MCHECKSUM_GPU_LOG2G", raising=False)
+            else:
+                monkeypatch.setenv("MCHECKSUM_GPU_LOG2G", str(lg))
+            # NT forces the large-batch kernels (CRC-32C aligned ones take the queue)
+            monkeypatch.setenv("MCHECKSUM_GPU_NT", str(int(rng.integers(0, 2))))
+            got = G.checksum_fixed(method, dev, length, count=count, stride=stride)
+            _wait(torch, (it, method, "fixed", length, stride, count, lg))
+            want = O.batch_fixed(method, host, stride, length, count, nthreads=8)
+            tag = ("fixed", length, stride, count, lg)
+        else:
+            count = int(rng.choice([1, 3, 16, 17, 100, 1025, 5000, 20000]))
+            lens = rng.integers(0, int(rng.choice([64, 4096, 65536])), count)
+            offs = np.zeros(count + 1, dtype=np.uint64)
+            offs[1:] = np.cumsum(lens)
+            if offs[-1] >= (64 << 20):
+                continue
+            offs += np.uint64(rng.integers(0, 16))
+            got = G.checksum_offsets(method, dev, torch.from_numpy(offs.astype(np.int64)).cuda(), offsets_host=offs)
+            _wait(torch, (it, method, "offsets", count))
+            want = O.batch_offsets(method, host, offs, nthreads=8)
+            tag = ("offsets", count)
+        g = G.as_unsigned(got).astype(np.uint64)
+        nb = int(np.count_nonzero(g != want))
+        if nb:
+            bad += 1
+            print("MISMATCH", it, method, tag, nb, flush=True)
+        if it % 50 == 0:
+            print(f"iter {it} ok ({time.time() - t0:.1f} s)", flush=True)
+    faults = G.queue_faults()
+    print(f"done {n_iter} launches, {bad} mismatching, queue faults {faults}", flush=True)
+    assert bad == 0 and faults == 0

@@ -56,10 +56,12 @@ def main():
     names = [os.path.basename(p)[len("libmchecksum_"):-3] for p in paths]
     libs = [load(p) for p in paths]
     envs = [None] * len(libs)
-    for spec in args.env:
+    for spec in args.env:  # NAME=VAR=VALUE[@variant]: a library run with VAR=VALUE set around its calls
+        spec, _, base = spec.partition("@")
         nm, var, val = spec.split("=", 2)
         names.append(nm)
-        libs.append(load(os.path.join(ROOT, "mercury_amd", "lib", "libmchecksum.so")))
+        libs.append(load(os.path.join(ROOT, "build", "variants", f"libmchecksum_{base}.so") if base
+                         else os.path.join(ROOT, "mercury_amd", "lib", "libmchecksum.so")))
         envs.append((var, val))
 
     results = {}
