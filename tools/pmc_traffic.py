@@ -5,7 +5,9 @@
 in KiB; FETCH_SIZE reads exactly half the bytes of a wide coalesced streaming
 read on gfx950, so it is doubled.
 
-usage: pmc_traffic.py FETCH_DIR WRITE_DIR KERNEL_SUBSTRING OUT_JSON [alg_bytes]
+usage: pmc_traffic.py FETCH_DIR WRITE_DIR KERNEL_SUBSTRING OUT_JSON [alg_bytes [dispatches_per_call]]
+(dispatches_per_call: kernels matching the substring per API call, e.g. 3 for
+the segments path: scan + two chunk passes)
 """
 import csv
 import glob
@@ -27,13 +29,14 @@ def read(d, counter, ksub):
 def main():
     fdir, wdir, ksub, out = sys.argv[1:5]
     alg = float(sys.argv[5]) if len(sys.argv) > 5 else None
+    per_call = int(sys.argv[6]) if len(sys.argv) > 6 else 1
     f = read(fdir, "FETCH_SIZE", ksub)
     w = read(wdir, "WRITE_SIZE", ksub)
     if not f or not w:
         raise SystemExit(f"no counter rows for {ksub!r}: fetch={len(f)} write={len(w)}")
-    fetch_b = 2 * 1024 * sum(f) / len(f)
-    write_b = 1024 * sum(w) / len(w)
-    res = {"kernel": ksub, "dispatches": {"fetch": len(f), "write": len(w)},
+    fetch_b = 2 * 1024 * sum(f) / len(f) * per_call
+    write_b = 1024 * sum(w) / len(w) * per_call
+    res = {"kernel": ksub, "dispatches": {"fetch": len(f), "write": len(w)}, "dispatches_per_call": per_call,
            "fetch_size_kib_raw_mean": sum(f) / len(f), "write_size_kib_mean": sum(w) / len(w),
            "hbm_read_bytes_per_launch": fetch_b, "hbm_write_bytes_per_launch": write_b,
            "hbm_bytes_per_launch": fetch_b + write_b,
