@@ -154,7 +154,10 @@ constexpr uint32_t kQSlotWords = (2 * kQSub + 1) * kQStride;
 // the current one is left to take: early enough to hide the fetch (~1.3 us
 // mean), late enough that a workgroup holds little unstarted work when the
 // queue runs dry.
-constexpr uint32_t kWgChunkMaxLog2 = 5;
+#ifndef MCK_QCHUNK_MAX_LOG2
+#define MCK_QCHUNK_MAX_LOG2 5
+#endif
+constexpr uint32_t kWgChunkMaxLog2 = MCK_QCHUNK_MAX_LOG2;
 // Which batches take the queue (profiles/r01/ab12_work_queue.log, medians
 // vs the static split): variable-length (offsets) batches, +4% C4 and +8%
 // C4-layout CRC-64 over the byte-balanced static split, and the large
@@ -290,7 +293,10 @@ __device__ __forceinline__ void for_each_unit(WgQueue *L, unsigned long long *qu
                                               uint32_t nw, F &&body) {
     if constexpr (DYN) {
         const bool l0 = (threadIdx.x & 63u) == 0;
-        const uint32_t cl = chunk_log2(n), cu = 1u << cl, lead = cu > 4 ? cu / 4 : 1;
+#ifndef MCK_QLEAD_DIV
+#define MCK_QLEAD_DIV 4
+#endif
+        const uint32_t cl = chunk_log2(n), cu = 1u << cl, lead = cu > MCK_QLEAD_DIV ? cu / MCK_QLEAD_DIV : 1;
         const uint64_t nch = (n + cu - 1) >> cl;
 #if MCK_TRACE
         unsigned long long qs_n = 0, qs_sum = 0, qs_max = 0, qs_wait = 0, qs_busy = 0, qs_units = 0;
