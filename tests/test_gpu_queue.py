@@ -77,3 +77,39 @@ def test_dynamic_queue_random_shapes(gpu, oracle_mod, n_iter, monkeypatch):
     faults = G.queue_faults()
     print(f"done {n_iter} launches, {bad} mismatching, queue faults {faults}", flush=True)
     assert bad == 0 and faults == 0
+
+
+def test_queue_slot_survives_graph_replay(gpu, oracle_mod, monkeypatch):
+    """A captured call keeps its work-queue slot; the last wave re-zeroes it, so
+    every replay distributes the whole batch again (offsets batch + an NT
+    fixed batch, both on the queue)."""
+    import torch
+    G, O = gpu, oracle_mod
+    monkeypatch.setenv("MCHECKSUM_GPU_LIGHT", "0")
+    monkeypatch.setenv("MCHECKSUM_GPU_NT", "1")
+    host = O.splitmix_bytes(8 << 20, 4242)
+    dev = torch.cat([torch.from_numpy(host).cuda(), torch.zeros(64, dtype=torch.uint8, device="cuda")])
+    rng = np.random.default_rng(7)
+    offs = np.zeros(3001, dtype=np.uint64)
+    offs[1:] = np.cumsum(rng.integers(0, 2048, 3000))
+    offs_d = torch.from_numpy(offs.astype(np.int64)).cuda()
+    G.prepare("crc32c")
+    out_o = torch.zeros(3000, dtype=torch.int32, device="cuda")
+    out_f = torch.zeros(2048, dtype=torch.int32, device="cuda")
+    G.checksum_offsets("crc32c", dev, offs_d, out=out_o, offsets_host=offs)  # validate once, eager
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s), torch.cuda.graph(g, stream=s):
+        G.checksum_offsets("crc32c", dev, offs_d, out=out_o)
+        G.checksum_fixed("crc32c", dev, 4096, count=2048, out=out_f)
+    want_o = O.batch_offsets("crc32c", host, offs, nthreads=8)
+    want_f = O.batch_fixed("crc32c", host, 4096, 4096, 2048, nthreads=8)
+    for _ in range(4):
+        out_o.zero_()
+        out_f.zero_()
+        g.replay()
+        _wait(torch, "graph replay")
+        assert np.array_equal(G.as_unsigned(out_o).astype(np.uint64), want_o)
+        assert np.array_equal(G.as_unsigned(out_f).astype(np.uint64), want_f)
+    assert G.queue_faults() == 0
