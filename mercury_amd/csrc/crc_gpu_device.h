@@ -272,7 +272,7 @@ __device__ void wg_publish(WgQueue *L, uint32_t seq, uint64_t id, uint32_t cl) {
 
 // Thread 0, before the kernel's first barrier: reset the LDS state and
 // publish the first chunk (its fetch overlaps the LDS table fill).
-__device__ void wg_queue_init(WgQueue *L, unsigned long long *q, uint64_t n) {
+__device__ __attribute__((unused)) void wg_queue_init(WgQueue *L, unsigned long long *q, uint64_t n) {
     L->slot = 0;
     L->drained = 0;
     L->exited = 0;

@@ -34,7 +34,7 @@ constexpr uint32_t kQueueSlots = 4096;
 extern std::mutex g_mu;
 
 // Record a formatted error for mchecksum_gpu_last_error(); returns rc.
-int set_err(int rc, const char *fmt, const char *a = "", int b = 0);
+int set_err(int rc, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
 int hip_err(hipError_t e, const char *what);
 // Method -> model index for GPU batch kernels (reflected 32/64-bit): -1 unknown, -2 no kernel.
 int gpu_model(const char *method, int *width);

@@ -26,6 +26,7 @@
 // No MFMA: this is HBM-bound byte scanning; the roofline is HBM read bandwidth.
 #include <hip/hip_runtime.h>
 
+#include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -41,8 +42,11 @@ namespace mck {
 
 thread_local char t_err[256] = "";
 
-int set_err(int rc, const char *fmt, const char *a, int b) {
-    snprintf(t_err, sizeof(t_err), fmt, a, b);
+int set_err(int rc, const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(t_err, sizeof(t_err), fmt, ap);
+    va_end(ap);
     return rc;
 }
 
@@ -68,7 +72,7 @@ int device_ctx(DevCtx **out) {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return hip_err(e, "hipGetDevice");
-    if (dev < 0 || dev >= kMaxDev) return set_err(MCHECKSUM_GPU_ENODEV, "device id %s%d out of range", "", dev);
+    if (dev < 0 || dev >= kMaxDev) return set_err(MCHECKSUM_GPU_ENODEV, "device id %d out of range", dev);
     DevCtx &c = g_dev[dev];
     if (!c.init) {
         int cus = 0;
@@ -115,7 +119,7 @@ int get_pack(DevCtx *c, int idx, int log2g, const void **pack) {
     }
     if (rc != 0) {
         free(host);
-        return set_err(MCHECKSUM_GPU_EINVAL, "table build failed for %s%d", m.name, log2g);
+        return set_err(MCHECKSUM_GPU_EINVAL, "table build failed for %s (G = %d)", m.name, 1 << log2g);
     }
     void *d = nullptr;
     hipError_t e = hipMalloc(&d, bytes);
@@ -233,8 +237,8 @@ unsigned grid_for(const DevCtx *c, uint64_t waves_needed, const KLaunch &kl) {
 
 int prologue(const char *method, int log2g, int *width, DevCtx **c, const void **pack) {
     int idx = gpu_model(method, width);
-    if (idx == -1) return set_err(MCHECKSUM_GPU_EMETHOD, "unknown hash method \"%s\"%d", method ? method : "(null)");
-    if (idx < 0) return set_err(MCHECKSUM_GPU_EMETHOD, "method \"%s\" has no GPU kernel (reflected 32/64-bit only)%d", method);
+    if (idx == -1) return set_err(MCHECKSUM_GPU_EMETHOD, "unknown hash method \"%s\"", method ? method : "(null)");
+    if (idx < 0) return set_err(MCHECKSUM_GPU_EMETHOD, "method \"%s\" has no GPU kernel (reflected 32/64-bit only)", method);
     std::lock_guard<std::mutex> lk(g_mu);
     int rc = device_ctx(c);
     if (rc) return rc;
@@ -248,11 +252,11 @@ int do_offsets(const char *method, const void *base, const uint64_t *offsets, si
                const void *expected, uint8_t *status, uint32_t *mism, void *stream, bool verify,
                bool msg = false, size_t pay_off = 0, size_t hash_off = 0) {
     if ((!base && count) || !offsets || (!verify && !out && count) || (verify && !msg && !expected))
-        return set_err(MCHECKSUM_GPU_EINVAL, "NULL pointer argument%s%d");
+        return set_err(MCHECKSUM_GPU_EINVAL, "NULL pointer argument");
     if (msg && (hash_off + 4 > pay_off || pay_off > (1u << 30)))
-        return set_err(MCHECKSUM_GPU_EINVAL, "hash_offset + 4 must not exceed payload_offset%s%d");
-    if ((uint64_t)count > kMaxUnits) return set_err(MCHECKSUM_GPU_EINVAL, "more than 2^32 - 2 payloads in one call%s%d");
-    if (!mchecksum_gpu_available()) return set_err(MCHECKSUM_GPU_ENODEV, "no HIP device%s%d");
+        return set_err(MCHECKSUM_GPU_EINVAL, "hash_offset + 4 must not exceed payload_offset");
+    if ((uint64_t)count > kMaxUnits) return set_err(MCHECKSUM_GPU_EINVAL, "more than 2^32 - 2 payloads in one call");
+    if (!mchecksum_gpu_available()) return set_err(MCHECKSUM_GPU_ENODEV, "no HIP device");
     int width = 0;
     DevCtx *c = nullptr;
     const void *pack = nullptr;
@@ -273,7 +277,7 @@ int do_offsets(const char *method, const void *base, const uint64_t *offsets, si
     a.hash_off = (uint32_t)hash_off;
     a.queue = nullptr;
     if (msg && width != 32)
-        return set_err(MCHECKSUM_GPU_EMETHOD, "message verify carries a 32-bit header hash: crc32c only%s%d");
+        return set_err(MCHECKSUM_GPU_EMETHOD, "message verify carries a 32-bit header hash: crc32c only");
     KLaunch k;
     // The offsets table stays on the device, so size the batch by its count:
     // 8192+ payloads of the C4 mix are ~270 MB and up.
@@ -330,7 +334,7 @@ int mchecksum_gpu_available(void) {
 }
 
 int mchecksum_gpu_prepare(const char *hash_method) {
-    if (!mchecksum_gpu_available()) return set_err(MCHECKSUM_GPU_ENODEV, "no HIP device%s%d");
+    if (!mchecksum_gpu_available()) return set_err(MCHECKSUM_GPU_ENODEV, "no HIP device");
     for (int lg = 0; lg <= CRC_GPU_MAX_LOG2G; lg++) {
         int width = 0;
         DevCtx *c = nullptr;
@@ -349,10 +353,10 @@ int mchecksum_gpu_lanes_per_payload(const char *hash_method, size_t len) {
 
 int mchecksum_gpu_checksum_fixed(const char *hash_method, const void *dev_base, size_t stride, size_t len,
                                  size_t count, void *dev_out, void *stream) {
-    if (count && (!dev_base || !dev_out)) return set_err(MCHECKSUM_GPU_EINVAL, "NULL pointer argument%s%d");
-    if (count > 1 && stride < len) return set_err(MCHECKSUM_GPU_EINVAL, "stride smaller than len%s%d");
-    if ((uint64_t)count > kMaxUnits) return set_err(MCHECKSUM_GPU_EINVAL, "more than 2^32 - 2 payloads in one call%s%d");
-    if (!mchecksum_gpu_available()) return set_err(MCHECKSUM_GPU_ENODEV, "no HIP device%s%d");
+    if (count && (!dev_base || !dev_out)) return set_err(MCHECKSUM_GPU_EINVAL, "NULL pointer argument");
+    if (count > 1 && stride < len) return set_err(MCHECKSUM_GPU_EINVAL, "stride smaller than len");
+    if ((uint64_t)count > kMaxUnits) return set_err(MCHECKSUM_GPU_EINVAL, "more than 2^32 - 2 payloads in one call");
+    if (!mchecksum_gpu_available()) return set_err(MCHECKSUM_GPU_ENODEV, "no HIP device");
     int width = 0;
     if (gpu_model(hash_method, &width) >= 0 && width == 32 && use_light((uint64_t)len * count, true)) {
         const int lg = light_log2g(len);

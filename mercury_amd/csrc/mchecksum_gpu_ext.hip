@@ -377,7 +377,7 @@ static int get_ext(DevCtx *c, int idx, const void **out) {
     }
     if (rc != 0) {
         free(host);
-        return set_err(MCHECKSUM_GPU_EINVAL, "table build failed for %s%d", m.name);
+        return set_err(MCHECKSUM_GPU_EINVAL, "table build failed for %s", m.name);
     }
     void *d = nullptr;
     hipError_t e = hipMalloc(&d, bytes);
@@ -404,10 +404,10 @@ int mchecksum_gpu_checksum_segments(const char *hash_method, const uint64_t *dev
                                     const uint64_t *dev_seg_len, size_t nseg, const uint64_t *dev_obj_first,
                                     size_t nobj, void *dev_work, size_t work_size, void *dev_out, void *stream) {
     if (!dev_obj_first || (nobj && !dev_out) || (nseg && (!dev_seg_addr || !dev_seg_len)) || !dev_work)
-        return set_err(MCHECKSUM_GPU_EINVAL, "NULL pointer argument%s%d");
+        return set_err(MCHECKSUM_GPU_EINVAL, "NULL pointer argument");
     if (work_size < mchecksum_gpu_segments_work_size(nseg) || (uintptr_t)dev_work % 8)
-        return set_err(MCHECKSUM_GPU_EINVAL, "workspace smaller than mchecksum_gpu_segments_work_size() or unaligned%s%d");
-    if (!mchecksum_gpu_available()) return set_err(MCHECKSUM_GPU_ENODEV, "no HIP device%s%d");
+        return set_err(MCHECKSUM_GPU_EINVAL, "workspace smaller than mchecksum_gpu_segments_work_size() or unaligned");
+    if (!mchecksum_gpu_available()) return set_err(MCHECKSUM_GPU_ENODEV, "no HIP device");
     int width = 0;
     DevCtx *c = nullptr;
     const void *pack = nullptr, *shift = nullptr;
@@ -453,17 +453,17 @@ int mchecksum_gpu_checksum_segments(const char *hash_method, const uint64_t *dev
 int mchecksum_gpu_verify_core_headers(const char *hash_method, int kind, const void *dev_buf,
                                       const uint64_t *dev_msg_offsets, size_t count, uint8_t *dev_status,
                                       uint32_t *dev_mismatches, void *stream) {
-    if ((count && !dev_buf) || !dev_msg_offsets) return set_err(MCHECKSUM_GPU_EINVAL, "NULL pointer argument%s%d");
+    if ((count && !dev_buf) || !dev_msg_offsets) return set_err(MCHECKSUM_GPU_EINVAL, "NULL pointer argument");
     if (kind != MCHECKSUM_GPU_CORE_HEADER_REQUEST && kind != MCHECKSUM_GPU_CORE_HEADER_RESPONSE)
-        return set_err(MCHECKSUM_GPU_EINVAL, "unknown core header kind %s%d", "", kind);
+        return set_err(MCHECKSUM_GPU_EINVAL, "unknown core header kind %d", kind);
     const int idx = mck_model_index(hash_method);
     if (idx < 0)
-        return set_err(MCHECKSUM_GPU_EMETHOD, "unknown hash method \"%s\"%d", hash_method ? hash_method : "(null)");
+        return set_err(MCHECKSUM_GPU_EMETHOD, "unknown hash method \"%s\"", hash_method ? hash_method : "(null)");
     const mck_model_t &m = mck_models[idx];
     if (m.width != 16)
-        return set_err(MCHECKSUM_GPU_EMETHOD, "core headers carry a 16-bit hash: \"%s\" is not a crc16 model%d",
+        return set_err(MCHECKSUM_GPU_EMETHOD, "core headers carry a 16-bit hash: \"%s\" is not a crc16 model",
                        hash_method);
-    if (!mchecksum_gpu_available()) return set_err(MCHECKSUM_GPU_ENODEV, "no HIP device%s%d");
+    if (!mchecksum_gpu_available()) return set_err(MCHECKSUM_GPU_ENODEV, "no HIP device");
     DevCtx *c = nullptr;
     const void *table = nullptr;
     {
