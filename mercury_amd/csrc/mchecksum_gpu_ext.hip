@@ -52,67 +52,144 @@ struct SegArgs {
     const uint64_t *first;
     uint64_t nobj;
     const uint64_t *P, *C;  // workspace: byte / chunk exclusive prefix sums, nseg + 1 each
+    const unsigned long long *ragged;  // workspace: non-zero if any chunk needs the ragged loop
     void *out;
     const void *pack, *shift;
 };
 
-// Exclusive prefix sums of segment bytes (P) and chunk counts (C) -- one
-// 1024-thread workgroup, 8 consecutive segments per thread per tile.
-__global__ __launch_bounds__(1024) void seg_scan_kernel(const uint64_t *len, uint64_t nseg, uint64_t *P, uint64_t *C) {
-    __shared__ uint64_t wp[16], wc[16];
-    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
-    uint64_t carry_p = 0, carry_c = 0;
-    for (uint64_t base = 0; base < nseg; base += 8192) {
-        uint64_t lp[8], lc[8], sp = 0, sc = 0;
+// Exclusive prefix sums of segment bytes (P) and chunk counts (C) in three
+// short launches over blocks of kScanBlk segments (one workgroup streams only
+// ~20 GB/s, so a single-workgroup scan of 32768 segments took 48 us):
+// reduce (block totals; also zeroes the output the chunk passes XOR into),
+// top (exclusive scan of the block totals, one workgroup) and down (block-local
+// scan + block offset).  The totals also count segments whose chunks cannot
+// all take the aligned loop (start not 16-B aligned or length not a multiple
+// of 1 KiB): the CRC-64 ragged pass returns at once when there are none.
+constexpr uint32_t kScanThreads = 256, kScanPer = 4, kScanBlk = kScanThreads * kScanPer;
+
+__device__ __forceinline__ uint64_t seg_chunks(uint64_t l) { return (l + kChunk - 1) / kChunk; }
+
+// Block-wide inclusive scan of (p, c) over 256 threads; returns the block
+// totals through *tp, *tc.
+__device__ __forceinline__ void block_scan2(uint64_t &p, uint64_t &c, uint64_t *tp, uint64_t *tc) {
+    __shared__ uint64_t wp[4], wc[4];
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
 #pragma unroll
-        for (int e = 0; e < 8; e++) {
-            const uint64_t i = base + t * 8u + e;
-            const uint64_t l = i < nseg ? len[i] : 0;
-            lp[e] = sp;
-            lc[e] = sc;
-            sp += l;
-            sc += (l + kChunk - 1) / kChunk;
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t op = __shfl_up(p, d, 64), oc = __shfl_up(c, d, 64);
+        if (lane >= (uint32_t)d) {
+            p += op;
+            c += oc;
         }
-        // inclusive wave scan of the thread sums
-        uint64_t ip = sp, ic = sc;
+    }
+    if (lane == 63) {
+        wp[w] = p;
+        wc[w] = c;
+    }
+    __syncthreads();
+    uint64_t bp = 0, bc = 0, sp = 0, sc = 0;
 #pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint64_t op = __shfl_up(ip, d, 64), oc = __shfl_up(ic, d, 64);
-            if (lane >= (uint32_t)d) {
-                ip += op;
-                ic += oc;
-            }
+    for (uint32_t v = 0; v < kScanThreads / 64; v++) {
+        if (v < w) {
+            bp += wp[v];
+            bc += wc[v];
         }
-        if (lane == 63) {
-            wp[w] = ip;
-            wc[w] = ic;
-        }
-        __syncthreads();
-        uint64_t bp = 0, bc = 0, tp = 0, tc = 0;  // waves before mine, tile total
-        for (uint32_t v = 0; v < 16; v++) {
-            if (v < w) {
-                bp += wp[v];
-                bc += wc[v];
-            }
-            tp += wp[v];
-            tc += wc[v];
-        }
-        const uint64_t ep = carry_p + bp + ip - sp, ec = carry_c + bc + ic - sc;  // exclusive, this thread
+        sp += wp[v];
+        sc += wc[v];
+    }
+    p += bp;
+    c += bc;
+    *tp = sp;
+    *tc = sc;
+}
+
+__global__ __launch_bounds__(kScanThreads) void seg_scan_reduce(const uint64_t *len, const uint64_t *addr, uint64_t nseg,
+                                                                uint64_t nb, uint64_t *tot, uint32_t *out,
+                                                                uint64_t out_words) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kScanThreads + threadIdx.x; i < out_words; i += (uint64_t)gridDim.x * kScanThreads)
+        out[i] = 0;
+    uint64_t p = 0, c = 0, r = 0;
 #pragma unroll
-        for (int e = 0; e < 8; e++) {
-            const uint64_t i = base + t * 8u + e;
-            if (i < nseg) {
-                P[i] = ep + lp[e];
-                C[i] = ec + lc[e];
-            }
+    for (uint32_t e = 0; e < kScanPer; e++) {
+        const uint64_t i = (uint64_t)blockIdx.x * kScanBlk + threadIdx.x * kScanPer + e;
+        if (i < nseg) {
+            const uint64_t l = len[i];
+            p += l;
+            c += seg_chunks(l);
+            r |= l && (l % 1024 != 0 || addr[i] % 16 != 0);
+        }
+    }
+    uint64_t tp, tc;
+    r = __any(r) ? 1 : 0;
+    block_scan2(p, c, &tp, &tc);
+    __shared__ uint32_t rag;
+    if (threadIdx.x == 0) rag = 0;
+    __syncthreads();
+    if (r && (threadIdx.x & 63u) == 0) atomicOr(&rag, 1u);
+    __syncthreads();
+    if (threadIdx.x == 0 && blockIdx.x < nb) {
+        tot[3 * blockIdx.x] = tp;
+        tot[3 * blockIdx.x + 1] = tc;
+        tot[3 * blockIdx.x + 2] = rag;
+    }
+}
+
+// One workgroup: block totals -> exclusive block offsets (in place); the
+// grand totals into P[nseg], C[nseg] and the ragged flag.
+__global__ __launch_bounds__(kScanThreads) void seg_scan_top(uint64_t *tot, uint64_t nb, uint64_t nseg, uint64_t *P,
+                                                             uint64_t *C, unsigned long long *ragged) {
+    uint64_t carry_p = 0, carry_c = 0, rag = 0;
+    for (uint64_t base = 0; base < nb; base += kScanThreads) {
+        const uint64_t b = base + threadIdx.x;
+        uint64_t p = b < nb ? tot[3 * b] : 0, c = b < nb ? tot[3 * b + 1] : 0;
+        rag |= b < nb ? tot[3 * b + 2] : 0;
+        const uint64_t p0 = p, c0 = c;
+        uint64_t tp, tc;
+        block_scan2(p, c, &tp, &tc);
+        if (b < nb) {
+            tot[3 * b] = carry_p + p - p0;
+            tot[3 * b + 1] = carry_c + c - c0;
         }
         carry_p += tp;
         carry_c += tc;
         __syncthreads();
     }
-    if (t == 0) {
+    rag = __any(rag) ? 1 : 0;
+    __shared__ uint32_t r;
+    if (threadIdx.x == 0) r = 0;
+    __syncthreads();
+    if (rag && (threadIdx.x & 63u) == 0) atomicOr(&r, 1u);
+    __syncthreads();
+    if (threadIdx.x == 0) {
         P[nseg] = carry_p;
         C[nseg] = carry_c;
+        *ragged = r;
+    }
+}
+
+__global__ __launch_bounds__(kScanThreads) void seg_scan_down(const uint64_t *len, uint64_t nseg, const uint64_t *tot,
+                                                              uint64_t *P, uint64_t *C) {
+    uint64_t l[kScanPer], p = 0, c = 0;
+#pragma unroll
+    for (uint32_t e = 0; e < kScanPer; e++) {
+        const uint64_t i = (uint64_t)blockIdx.x * kScanBlk + threadIdx.x * kScanPer + e;
+        l[e] = i < nseg ? len[i] : 0;
+        p += l[e];
+        c += seg_chunks(l[e]);
+    }
+    const uint64_t p0 = p, c0 = c;
+    uint64_t tp, tc;
+    block_scan2(p, c, &tp, &tc);
+    uint64_t ep = tot[3 * blockIdx.x] + p - p0, ec = tot[3 * blockIdx.x + 1] + c - c0;
+#pragma unroll
+    for (uint32_t e = 0; e < kScanPer; e++) {
+        const uint64_t i = (uint64_t)blockIdx.x * kScanBlk + threadIdx.x * kScanPer + e;
+        if (i < nseg) {
+            P[i] = ep;
+            C[i] = ec;
+        }
+        ep += l[e];
+        ec += seg_chunks(l[e]);
     }
 }
 
@@ -188,17 +265,42 @@ struct ChunkWalk {
     }
 };
 
+// Each object's Z^N(init) ^ xorout term (N = its byte count), XORed into
+// out[j] next to the chunk terms.  Latency-bound (up to 12 dependent table
+// applications per object), no LDS: the CRC-64 ragged pass runs only this when
+// no chunk needs the ragged loop.
+template <int W>
+__device__ __forceinline__ void seg_object_terms(const SegArgs &a) {
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < a.nobj; j += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t N = a.P[a.first[j + 1]] - a.P[a.first[j]];
+        if constexpr (W == 32) {
+            const crc32_gpu_pack_t *pk = reinterpret_cast<const crc32_gpu_pack_t *>(a.pack);
+            const crc32_shift_pack_t *sp = reinterpret_cast<const crc32_shift_pack_t *>(a.shift);
+            atomicXor(reinterpret_cast<uint32_t *>(a.out) + j, shift32(sp, pk->init, N) ^ pk->xorout);
+        } else {
+            const crc64_gpu_pack_t *pk = reinterpret_cast<const crc64_gpu_pack_t *>(a.pack);
+            const crc64_shift_pack_t *sp = reinterpret_cast<const crc64_shift_pack_t *>(a.shift);
+            atomicXor(reinterpret_cast<unsigned long long *>(a.out) + j,
+                      (unsigned long long)(shift64(sp, pk->init, N) ^ pk->xorout));
+        }
+    }
+}
+
 // PART 0: every chunk + the object terms (CRC-32C: 140 KiB of LDS, one
 // workgroup per CU either way).  CRC-64 splits the chunks by shape: PART 1
 // takes the aligned ones with two workgroups per CU (8 waves/SIMD: the
 // VALU/LDS-bound loop needs them, and <= 64 VGPRs only fits the aligned
-// loop), PART 2 the ragged ones and the object terms.
+// loop), PART 2 the ragged ones (if any) and the object terms.
 // (keyed W * 4 + PART: a comma inside __launch_bounds__ splits the macro)
 template <int KEY>
 constexpr int kSegWavesPerEU = KEY == 64 * 4 + 1 ? 8 : 1;
 
 template <int W, int PART>
 __global__ __launch_bounds__(1024, kSegWavesPerEU<W * 4 + PART>) void seg_kernel(SegArgs a) {
+    if (PART == 2 && *a.ragged == 0) {  // every chunk took the aligned pass: object terms only
+        seg_object_terms<W>(a);
+        return;
+    }
     constexpr int kWPB = 1024 / 64;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWPB + (threadIdx.x >> 6));
@@ -227,10 +329,7 @@ __global__ __launch_bounds__(1024, kSegWavesPerEU<W * 4 + PART>) void seg_kernel
             x = shift32(sp, uniform(x), after);
             if (lane == 0) atomicXor(out + j, x);
         }
-        for (uint64_t j = (uint64_t)blockIdx.x * 1024 + threadIdx.x; j < a.nobj; j += (uint64_t)gridDim.x * 1024) {
-            const uint64_t N = a.P[a.first[j + 1]] - a.P[a.first[j]];
-            atomicXor(out + j, shift32(sp, pk->init, N) ^ pk->xorout);
-        }
+        seg_object_terms<32>(a);
     } else {
         __shared__ __attribute__((aligned(16))) uint8_t lds[kL64Bytes];
         const crc64_gpu_pack_t *pk = reinterpret_cast<const crc64_gpu_pack_t *>(a.pack);
@@ -256,10 +355,7 @@ __global__ __launch_bounds__(1024, kSegWavesPerEU<W * 4 + PART>) void seg_kernel
             if (lane == 0) atomicXor(out + j, (unsigned long long)x);
         }
         if constexpr (PART == 1) return;
-        for (uint64_t j = (uint64_t)blockIdx.x * 1024 + threadIdx.x; j < a.nobj; j += (uint64_t)gridDim.x * 1024) {
-            const uint64_t N = a.P[a.first[j + 1]] - a.P[a.first[j]];
-            atomicXor(out + j, (unsigned long long)(shift64(sp, pk->init, N) ^ pk->xorout));
-        }
+        seg_object_terms<64>(a);
     }
 }
 
@@ -398,7 +494,10 @@ using namespace mck;
 
 extern "C" {
 
-size_t mchecksum_gpu_segments_work_size(size_t nseg) { return 2 * sizeof(uint64_t) * (nseg + 1); }
+// P, C (nseg + 1 each), the ragged flag (+ pad), 3 words per scan block.
+size_t mchecksum_gpu_segments_work_size(size_t nseg) {
+    return sizeof(uint64_t) * (2 * (nseg + 1) + 2 + 3 * ((nseg + kScanBlk - 1) / kScanBlk));
+}
 
 int mchecksum_gpu_checksum_segments(const char *hash_method, const uint64_t *dev_seg_addr,
                                     const uint64_t *dev_seg_len, size_t nseg, const uint64_t *dev_obj_first,
@@ -420,8 +519,6 @@ int mchecksum_gpu_checksum_segments(const char *hash_method, const uint64_t *dev
     if (rc) return rc;
     if (nobj == 0) return MCHECKSUM_GPU_OK;
     hipStream_t s = (hipStream_t)stream;
-    hipError_t e = hipMemsetAsync(dev_out, 0, nobj * (size_t)(width / 8), s);
-    if (e != hipSuccess) return hip_err(e, "hipMemsetAsync");
     SegArgs a{};
     a.addr = dev_seg_addr;
     a.len = dev_seg_len;
@@ -430,12 +527,24 @@ int mchecksum_gpu_checksum_segments(const char *hash_method, const uint64_t *dev
     a.nobj = nobj;
     a.P = (const uint64_t *)dev_work;
     a.C = (const uint64_t *)dev_work + (nseg + 1);
+    a.ragged = (const unsigned long long *)dev_work + 2 * (nseg + 1);
     a.out = dev_out;
     a.pack = pack;
     a.shift = shift;
-    hipLaunchKernelGGL(seg_scan_kernel, dim3(1), dim3(1024), 0, s, dev_seg_len, (uint64_t)nseg, (uint64_t *)a.P,
-                       (uint64_t *)a.C);
-    e = hipGetLastError();
+    const uint64_t nb = (nseg + kScanBlk - 1) / kScanBlk;
+    uint64_t *tot = (uint64_t *)dev_work + 2 * (nseg + 1) + 2;
+    const uint64_t out_words = (uint64_t)nobj * (uint64_t)(width / 32);
+    // at least one block per scan block, and enough to zero the output quickly
+    uint64_t zgrid = (out_words + kScanThreads - 1) / kScanThreads;
+    zgrid = zgrid > 1024 ? 1024 : zgrid;
+    const unsigned rgrid = (unsigned)(nb > zgrid ? nb : zgrid > 0 ? zgrid : 1);
+    hipLaunchKernelGGL(seg_scan_reduce, dim3(rgrid), dim3(kScanThreads), 0, s, dev_seg_len, dev_seg_addr,
+                       (uint64_t)nseg, nb, tot, (uint32_t *)dev_out, out_words);
+    hipLaunchKernelGGL(seg_scan_top, dim3(1), dim3(kScanThreads), 0, s, tot, nb, (uint64_t)nseg, (uint64_t *)a.P,
+                       (uint64_t *)a.C, (unsigned long long *)a.ragged);
+    if (nb) hipLaunchKernelGGL(seg_scan_down, dim3((unsigned)nb), dim3(kScanThreads), 0, s, dev_seg_len, (uint64_t)nseg,
+                               tot, (uint64_t *)a.P, (uint64_t *)a.C);
+    hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_err(e, "segment scan launch");
     if (width == 32) {
         hipLaunchKernelGGL((seg_kernel<32, 0>), dim3(c->cus), dim3(1024), 0, s, a);

@@ -190,3 +190,24 @@ def test_core_headers_reject_wide_methods(gpu):
         gpu.verify_core_headers(data, offs, method="crc32c")
     with pytest.raises(gpu.GpuChecksumError):
         gpu.verify_core_headers(data, offs, kind="reply")
+
+
+@pytest.mark.parametrize("method", ["crc32c", "crc64"])
+def test_segments_long_lists_multi_block_scan(gpu, buf, oracle_mod, method):
+    """300000 short segments (the prefix scan runs in 293 blocks, so its
+    block-offset pass takes two tiles) and an all-aligned list (every chunk on
+    the aligned pass: the CRC-64 ragged pass returns at once)."""
+    host = _host(buf)
+    rng = np.random.default_rng(91)
+    lens = rng.integers(0, 65, 300000)
+    offs = rng.integers(0, buf.numel() - 128, 300000)
+    first = list(range(0, 300001, 5))
+    views = [buf[int(o):int(o) + int(n)] for o, n in zip(offs, lens)]
+    got = gpu.as_unsigned(gpu.checksum_segments(method, views, first))
+    for j in list(range(0, 60000, 97)) + [59999]:
+        b = b"".join(host[int(offs[s]):int(offs[s]) + int(lens[s])].tobytes() for s in range(first[j], first[j + 1]))
+        assert int(got[j]) == oracle_mod.crc(method, np.frombuffer(b, dtype=np.uint8)), j
+    segs = [(16 * int(o), 4096) for o in rng.integers(0, (buf.numel() - 8192) // 16, 3000)]
+    first = list(range(0, 3001, 3))
+    got = gpu.as_unsigned(gpu.checksum_segments(method, [buf[o:o + n] for o, n in segs], first))
+    assert got.tolist() == _want(oracle_mod, method, host, segs, first)

@@ -25,6 +25,7 @@ SHAPES = {
     "c3": ("crc64", 8192, 1 << 20, 0x4D43310000000003),
     "c4": ("crc32c", 262144, None, 0x4D43310000000004),   # offsets table, U[64 B, 64 KiB]
     "c4_64": ("crc64", 262144, None, 0x4D43310000000004),
+    "seg": ("crc64", 8192, "seg", 0x4D43310000000003),      # bench.py's segments layout
 }
 
 
@@ -36,6 +37,8 @@ def load(path):
                                                c.c_void_p, c.c_void_p]
     L.mchecksum_gpu_checksum_offsets.argtypes = [c.c_char_p, c.c_void_p, c.c_void_p, c.c_size_t, c.c_void_p,
                                                  c.c_void_p]
+    L.mchecksum_gpu_checksum_segments.argtypes = [c.c_char_p, c.c_void_p, c.c_void_p, c.c_size_t, c.c_void_p,
+                                                  c.c_size_t, c.c_void_p, c.c_size_t, c.c_void_p, c.c_void_p]
     return L
 
 
@@ -68,8 +71,18 @@ def main():
     configs = args.config.split(",")
     for cfg in configs:
         method, count, length, seed = SHAPES[cfg]
-        offs = None
-        if length is None:
+        offs = seg = None
+        if length == "seg":
+            from mercury_amd.workload import segment_slots
+            nbytes, slen = count << 20, (1 << 20) // 4
+            data = torch.empty(nbytes + 64, dtype=torch.uint8, device="cuda")
+            G.fill_splitmix(data, seed)
+            slots = segment_slots(seed, count * 4)
+            seg = G.SegmentBatch([data[int(q) * slen:(int(q) + 1) * slen] for q in slots],
+                                 np.arange(0, count * 4 + 1, 4))
+            seg.work = torch.empty(seg.work.numel() + 64, dtype=torch.int64, device="cuda")  # room for any variant
+            ref = seg.checksum(method)
+        elif length is None:
             from mercury_amd.workload import varlen_offsets
             off_h = varlen_offsets(seed, count)
             nbytes = int(off_h[-1])
@@ -97,7 +110,11 @@ def main():
                        for _ in range(args.iters)]
                 for a, b in evs:
                     a.record(stream)
-                    if offs is None:
+                    if seg is not None:
+                        mb, ns = seg.meta.data_ptr(), seg.nseg
+                        rc = L.mchecksum_gpu_checksum_segments(method.encode(), mb, mb + 8 * ns, ns, mb + 16 * ns, seg.nobj,
+                                                               seg.work.data_ptr(), seg.work.numel() * 8, o.data_ptr(), h)
+                    elif offs is None:
                         rc = L.mchecksum_gpu_checksum_fixed(method.encode(), data.data_ptr(), length, length, count,
                                                             o.data_ptr(), h)
                     else:
