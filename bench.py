@@ -43,6 +43,10 @@ CONFIGS = {
     # C5: the 2^20 x 64 KiB global batch (64 GiB) split over the ranks --
     # strong scaling (8 GiB per GPU at 8 GPUs; all of it on one GPU at N=1)
     "c5": ("crc32c", 1 << 20, 65536, 0x4D43310000000005, "fixed"),
+    # 8(f) 1: C4's packets as Mercury messages (16 B core header, 4 B HG header
+    # carrying the network-order payload CRC, payload) verified in place --
+    # the batched hg_get_struct checksum check
+    "msgs": ("crc32c", 262144, None, 0x4D43310000000004, "messages"),
     # BASELINE configs[0]: host CPU, through the drop-in streaming API
     "c1": ("crc32c", 1024, 4096, 0x4D43310000000001, "cpu"),
 }
@@ -114,6 +118,30 @@ def main():
                                np.arange(0, count * SEGS_PER_OBJECT + 1, SEGS_PER_OBJECT))
         offsets_dev = offsets_host = None
         run = lambda out: batch.checksum(method, out=out)  # noqa: E731
+    elif layout == "messages":
+        from mercury_amd.workload import varlen_offsets
+        msg_host = varlen_offsets(seed ^ rank, count)
+        payload_bytes = int(msg_host[-1])
+        data = torch.empty(payload_bytes + 64, dtype=torch.uint8, device=dev)
+        G.fill_splitmix(data, seed ^ rank)
+        # sender side (hg_set_struct): CRC of each payload = message bytes
+        # [20, len); one offsets batch over the interleaved table
+        # (header_i, payload_i, ...), the checker's layout as well
+        offsets_host = np.empty(2 * count + 1, dtype=np.uint64)
+        offsets_host[0::2] = msg_host
+        offsets_host[1::2] = msg_host[:-1] + np.uint64(20)
+        sender = G.checksum_offsets(method, data, torch.from_numpy(offsets_host.astype(np.int64)).to(dev),
+                                    offsets_host=offsets_host)
+        # ... stored network-order in each message's HG header (bytes 16..19)
+        msg_dev = torch.from_numpy(msg_host.astype(np.int64)).to(dev)
+        crc = sender[1::2].to(torch.int64) & 0xFFFFFFFF
+        for k in range(4):
+            data[msg_dev[:-1] + 16 + k] = ((crc >> (24 - 8 * k)) & 0xFF).to(torch.uint8)
+        offsets_dev = msg_dev
+        status = torch.empty(count, dtype=torch.uint8, device=dev)
+        mism = torch.zeros(1, dtype=torch.int32, device=dev)
+        G.verify_messages(data, msg_dev, status=status, mismatches=mism, offsets_host=msg_host)  # validates once
+        run = lambda out: G.verify_messages(data, msg_dev, status=status, mismatches=mism)  # noqa: E731
     else:
         from mercury_amd.workload import varlen_offsets
         offsets_host = varlen_offsets(seed ^ rank, count)
@@ -153,6 +181,20 @@ def main():
 
     # ---- gathered result (outside the timed region) ----------------------
     crcs = out
+    verify_note = None
+    if layout == "messages":
+        # every timed verify passed (the mismatch counter accumulates over all
+        # launches), and one flipped payload bit is caught exactly where it is
+        bad_before = int(mism.item())
+        victim = count // 3
+        pos = int(msg_host[victim]) + 20 + (int(msg_host[victim + 1] - msg_host[victim]) - 20) // 2
+        data[pos] ^= 0x10
+        st, m2 = G.verify_messages(data, offsets_dev)
+        flagged = torch.nonzero(st).flatten().tolist()
+        data[pos] ^= 0x10
+        verify_note = (f"{args.steps + args.warmup + 1} verify launches: {bad_before} mismatches; one flipped bit "
+                       f"flagged {flagged} (expected [{victim}])")
+        crcs = sender  # the sender-side CRCs, checked against the oracle below
     if world > 1:
         mine = out.to(coll_dev)
         gathered = [torch.empty_like(mine) for _ in range(world)]
@@ -165,6 +207,8 @@ def main():
     out_bytes = count * (4 if G.out_dtype(method) == torch.int32 else 8)
     alg_bytes = payload_bytes + out_bytes + (8 * (count + 1) if layout == "offsets" else 0) + \
         (16 * count * SEGS_PER_OBJECT + 8 * (count + 1) if layout == "segments" else 0)
+    if layout == "messages":  # messages read (headers included), 1 status byte each, the offsets table
+        alg_bytes = payload_bytes + count + 8 * (count + 1)
     achieved = alg_bytes / (kern_ms_max * 1e-3) / 1e9
 
     result = None
@@ -192,6 +236,7 @@ def main():
             "data": "synthetic (splitmix64 bytes generated on device)",
             "config": {"workload": f"{method} over {count} x {length if length else 'U[64B,64KiB]'} B payloads per GPU"
                        + (" (offsets table)" if layout == "offsets" else "")
+                       + (" as Mercury messages, verified in place" if layout == "messages" else "")
                        + (f" ({SEGS_PER_OBJECT} scattered segments each)" if layout == "segments" else ""),
                        "method": method, "payloads_per_gpu": count, "payload_bytes": length,
                        "bytes_per_gpu": payload_bytes, "lanes_per_payload": G.lanes_per_payload(method, length or 65536)
@@ -206,11 +251,15 @@ def main():
             result["cpu_baseline"], result["parity"] = cpu_baseline(
                 method, seed, length, offsets_host, got, args.cpu_seconds, args.parity_samples,
                 segments=layout == "segments")
+        elif world > 1 and layout == "messages":
+            result["parity"] = "per-rank verify counters (see verify)"
         elif world > 1:
             result["parity"] = cross_rank_check(G, method, seed, length, offsets_host, got, count, world, dev,
                                                 args.parity_samples, segments=layout == "segments")
         else:
             result["parity"] = "unchecked (--no-cpu-baseline)"
+        if verify_note:
+            result["verify"] = verify_note
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.barrier()

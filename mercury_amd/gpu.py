@@ -148,15 +148,22 @@ def verify_offsets(method: str, data: torch.Tensor, offsets: torch.Tensor, expec
 
 
 def verify_messages(data: torch.Tensor, msg_offsets: torch.Tensor, payload_offset: int = 20, hash_offset: int = 16,
-                    method: str = "crc32c", stream=None, offsets_host=None):
+                    method: str = "crc32c", stream=None, offsets_host=None, status=None, mismatches=None):
     """Verify received RPC messages in place: payload after payload_offset,
     expected CRC = network-order u32 at hash_offset (Mercury: 16 B core header,
-    4 B HG header).  Returns (status uint8 per message: 1 = fails, count)."""
+    4 B HG header).  Returns (status uint8 per message: 1 = fails, count).
+    Pass preallocated `status` (uint8, >= count) and `mismatches` (int32, one
+    element, zeroed by the caller; the call adds to it) to reuse buffers."""
     _check_device_u8(data, "data")
     _check_offsets(data, msg_offsets, offsets_host)
     count = msg_offsets.numel() - 1
-    status = torch.empty(max(count, 0), dtype=torch.uint8, device=data.device)
-    mism = torch.zeros(1, dtype=torch.int32, device=data.device)
+    if status is None:
+        status = torch.empty(max(count, 0), dtype=torch.uint8, device=data.device)
+    elif status.dtype != torch.uint8 or status.numel() < count or not status.is_cuda:
+        raise GpuChecksumError("status must be a device uint8 tensor of at least count elements")
+    mism = torch.zeros(1, dtype=torch.int32, device=data.device) if mismatches is None else mismatches
+    if mism.dtype != torch.int32 or not mism.is_cuda:
+        raise GpuChecksumError("mismatches must be a device int32 tensor")
     rc = _lib().mchecksum_gpu_verify_messages(method.encode(), data.data_ptr(), msg_offsets.data_ptr(), count,
                                               payload_offset, hash_offset, status.data_ptr(), mism.data_ptr(),
                                               _stream_handle(stream))
