@@ -56,7 +56,8 @@ mchecksum_gpu_available(void);
 MCHECKSUM_PUBLIC int
 mchecksum_gpu_prepare(const char *hash_method);
 
-/* Fixed-size batch: payload i = dev_base[i*stride, i*stride + len), i < count. */
+/* Fixed-size batch: payload i = dev_base[i*stride, i*stride + len), i < count.
+ * (Every batch entry point takes at most 2^31 payloads per call.) */
 MCHECKSUM_PUBLIC int
 mchecksum_gpu_checksum_fixed(const char *hash_method, const void *dev_base,
     size_t stride, size_t len, size_t count, void *dev_out, void *stream);

@@ -246,7 +246,9 @@ int prologue(const char *method, int log2g, int *width, DevCtx **c, const void *
 }
 
 // The work queue's chunk ids are 32-bit (crc_gpu_device.h, WgQueue).
-constexpr uint64_t kMaxUnits = kNoChunk - 1;  // chunk ids < 2^32 even at one unit per chunk
+// The work queue counts chunk ids and per-workgroup slots in 32 bits
+// (crc_gpu_device.h, WgQueue): 2^31 payloads per call keeps both in range.
+constexpr uint64_t kMaxUnits = 1ull << 31;
 
 int do_offsets(const char *method, const void *base, const uint64_t *offsets, size_t count, void *out,
                const void *expected, uint8_t *status, uint32_t *mism, void *stream, bool verify,
@@ -255,7 +257,7 @@ int do_offsets(const char *method, const void *base, const uint64_t *offsets, si
         return set_err(MCHECKSUM_GPU_EINVAL, "NULL pointer argument");
     if (msg && (hash_off + 4 > pay_off || pay_off > (1u << 30)))
         return set_err(MCHECKSUM_GPU_EINVAL, "hash_offset + 4 must not exceed payload_offset");
-    if ((uint64_t)count > kMaxUnits) return set_err(MCHECKSUM_GPU_EINVAL, "more than 2^32 - 2 payloads in one call");
+    if ((uint64_t)count > kMaxUnits) return set_err(MCHECKSUM_GPU_EINVAL, "more than 2^31 payloads in one call");
     if (!mchecksum_gpu_available()) return set_err(MCHECKSUM_GPU_ENODEV, "no HIP device");
     int width = 0;
     DevCtx *c = nullptr;
@@ -355,7 +357,7 @@ int mchecksum_gpu_checksum_fixed(const char *hash_method, const void *dev_base, 
                                  size_t count, void *dev_out, void *stream) {
     if (count && (!dev_base || !dev_out)) return set_err(MCHECKSUM_GPU_EINVAL, "NULL pointer argument");
     if (count > 1 && stride < len) return set_err(MCHECKSUM_GPU_EINVAL, "stride smaller than len");
-    if ((uint64_t)count > kMaxUnits) return set_err(MCHECKSUM_GPU_EINVAL, "more than 2^32 - 2 payloads in one call");
+    if ((uint64_t)count > kMaxUnits) return set_err(MCHECKSUM_GPU_EINVAL, "more than 2^31 payloads in one call");
     if (!mchecksum_gpu_available()) return set_err(MCHECKSUM_GPU_ENODEV, "no HIP device");
     int width = 0;
     if (gpu_model(hash_method, &width) >= 0 && width == 32 && use_light((uint64_t)len * count, true)) {
