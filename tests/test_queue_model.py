@@ -1,0 +1,159 @@
+"""CPU model of the batch kernels' work-queue protocol (crc_gpu_device.h:
+WgQueue, wg_fetch, wg_publish, for_each_unit), run under random interleavings
+of every wave's shared-memory steps.  Checks what the GPU relies on: every
+unit is processed exactly once, no wait can block forever, and the last
+workgroup leaves the slot's counters at zero for the next launch.
+
+Each wave is a generator that yields at every access to shared state (LDS or
+the global slot), so a seeded scheduler explores many orders of the same
+steps the device code takes.  Fetch triggers, chunk sizes (chunk_log2), the
+round-robin sub-queues, the LDS ring recycling and the hierarchical exit
+counting mirror the device code one to one.
+"""
+import random
+
+import pytest
+
+QSUB, RING, NOCH = 8, 8, 0xFFFFFFFF
+
+
+def chunk_log2(n, grid, max_log2=5):
+    share = n // (4 * grid)
+    lg = 0
+    while lg < max_log2 and (2 << lg) <= share:
+        lg += 1
+    return lg
+
+
+class Slot:
+    def __init__(self):
+        self.sub = [0] * QSUB          # sub-queue tickets
+        self.group_done = [0] * QSUB   # exited workgroups per group
+        self.all_done = 0
+
+
+class Lds:
+    def __init__(self):
+        self.slot = 0
+        self.drained = 0
+        self.exited = 0
+        self.reads = [0] * RING
+        self.entry = [(0xFFFFFFFF, 0)] * RING
+
+
+def run_model(n, grid, waves_per_wg, seed, slot=None, max_steps=2_000_000):
+    rnd = random.Random(seed)
+    slot = slot or Slot()
+    cl = chunk_log2(n, grid)
+    cu, lead = 1 << cl, max(1, (1 << cl) // 4) if (1 << cl) > 4 else 1
+    nch = (n + cu - 1) >> cl
+    done_units = []
+    lds = [Lds() for _ in range(grid)]
+
+    def fetch(L, b):  # wg_fetch
+        home = b % QSUB
+        d = L.drained
+        while d < QSUB:
+            k = (home + d) % QSUB
+            t = slot.sub[k]
+            slot.sub[k] += 1
+            yield
+            if k + t * QSUB < nch:
+                return k + t * QSUB
+            L.drained = max(L.drained, d + 1)
+            yield
+            d = max(L.drained, d + 1)
+        return NOCH
+
+    def publish(L, seq, cid):  # wg_publish
+        r = seq % RING
+        if seq >= RING:
+            while L.reads[r] != cu:
+                yield
+        L.reads[r] = 0
+        yield
+        L.entry[r] = (seq, cid)
+        yield
+
+    def wave(b):  # for_each_unit<true>
+        L = lds[b]
+        while True:
+            t = L.slot
+            L.slot += 1
+            yield
+            seq, r = t >> cl, (t >> cl) % RING
+            while L.entry[r][0] != seq:
+                yield
+            e = L.entry[r]
+            L.reads[r] += 1
+            yield
+            if (t & (cu - 1)) == cu - lead:
+                nid = NOCH if e[1] == NOCH else (yield from fetch(L, b))
+                yield from publish(L, seq + 1, nid)
+            if e[1] == NOCH:
+                break
+            u = (e[1] << cl) + (t & (cu - 1))
+            if u < n:
+                done_units.append(u)
+                for _ in range(rnd.randint(0, 40)):
+                    yield
+        # hierarchical exit counting
+        L.exited += 1
+        yield
+        if L.exited == waves_per_wg:
+            g = b % QSUB
+            wgs = (grid - g + QSUB - 1) // QSUB
+            groups = min(grid, QSUB)
+            prev = slot.group_done[g]
+            slot.group_done[g] += 1
+            yield
+            if prev == wgs - 1:
+                prev_all = slot.all_done
+                slot.all_done += 1
+                yield
+                if prev_all == groups - 1:
+                    slot.sub = [0] * QSUB
+                    slot.group_done = [0] * QSUB
+                    slot.all_done = 0
+
+    # wg_queue_init (thread 0 of every workgroup, before the barrier)
+    for b in range(grid):
+        g = (lambda L=lds[b], b=b: (yield from publish(L, 0, (yield from fetch(L, b)))))()
+        for _ in g:
+            pass
+    gens = [wave(b) for b in range(grid) for _ in range(waves_per_wg)]
+    steps = 0
+    while gens:
+        g = rnd.choice(gens)
+        try:
+            next(g)
+        except StopIteration:
+            gens.remove(g)
+        steps += 1
+        assert steps < max_steps, "no progress: a wait never ends"
+    return sorted(done_units), slot
+
+
+@pytest.mark.parametrize("n,grid", [(1, 1), (2, 3), (17, 1), (67, 2), (67, 5), (100, 3), (257, 8), (1000, 9),
+                                    (4096, 1), (4096, 16), (20000, 8)])
+def test_every_unit_once_and_slot_reset(n, grid):
+    slot = Slot()
+    for seed in range(3):
+        units, slot = run_model(n, grid, 4, seed * 7919 + n, slot)  # the slot is reused, as by the next launch
+        assert units == list(range(n))
+        assert slot.sub == [0] * QSUB and slot.group_done == [0] * QSUB and slot.all_done == 0
+
+
+def test_chunk_size_rule():
+    # C4 (262144 units, 256 workgroups): 32-unit chunks; C3-sized fixed batch at
+    # 512 workgroups: 4; a small batch: single units
+    assert 1 << chunk_log2(262144, 256) == 32
+    assert 1 << chunk_log2(8192, 512) == 4
+    assert 1 << chunk_log2(100, 256) == 1
+
+
+@pytest.mark.parametrize("n,grid", [(67, 2), (5000, 4), (262144 // 64, 8)])
+def test_sixteen_waves_per_workgroup(n, grid):
+    units, slot = run_model(n, grid, 16, n + grid)
+    assert units == list(range(n))
+    assert slot.sub == [0] * QSUB and slot.all_done == 0
