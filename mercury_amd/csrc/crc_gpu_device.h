@@ -177,6 +177,33 @@ __device__ __forceinline__ uint32_t chunk_log2(uint64_t n) {
     while (l < kWgChunkMaxLog2 && (2ull << l) <= share) l++;
     return l;
 }
+
+// Chunk plan: ids [0, nbig) are full chunks of 2^cl units; the last
+// (about one full chunk per workgroup of) units go out as quarter chunks, ids
+// [nbig, nch), so a workgroup that fetches late holds little unstarted work
+// when the queue runs dry (MCK_QTAIL=0: full chunks throughout).  The highest
+// ids are handed out last (every sub-queue counts up), so the small chunks
+// form the tail.
+#ifndef MCK_QTAIL
+#define MCK_QTAIL 1
+#endif
+struct ChunkPlan {
+    uint32_t cl, sl;    // log2 of the full / tail chunk size
+    uint64_t nbig, nch, big_end;
+    __device__ __forceinline__ explicit ChunkPlan(uint64_t n) {
+        cl = chunk_log2(n);
+        sl = MCK_QTAIL && cl >= 2 ? cl - 2 : cl;
+        const uint64_t tail = (uint64_t)gridDim.x << cl;
+        nbig = n > tail ? (n - tail) >> cl : 0;
+        big_end = nbig << cl;
+        nch = nbig + ((n - big_end + (1ull << sl) - 1) >> sl);
+    }
+    // first unit and size of chunk id
+    __device__ __forceinline__ uint64_t start(uint64_t id) const {
+        return id < nbig ? id << cl : big_end + ((id - nbig) << sl);
+    }
+    __device__ __forceinline__ uint32_t size(uint64_t id) const { return id < nbig ? 1u << cl : 1u << sl; }
+};
 constexpr uint32_t kWgRing = 8;    // LDS ring of published chunk ids
 constexpr uint64_t kNoChunk = 0xFFFFFFFFull;
 
@@ -280,8 +307,8 @@ __device__ __attribute__((unused)) void wg_queue_init(WgQueue *L, unsigned long 
         L->reads[r] = 0;
         L->entry[r] = ~0ull;
     }
-    const uint32_t cl = chunk_log2(n);
-    wg_publish(L, 0, wg_fetch(L, q, (n + (1ull << cl) - 1) >> cl), cl);
+    const ChunkPlan plan(n);
+    wg_publish(L, 0, wg_fetch(L, q, plan.nch), plan.cl);
 }
 
 // Calls body(u) for this wave's units: through the work queue (DYN: the
@@ -296,8 +323,9 @@ __device__ __forceinline__ void for_each_unit(WgQueue *L, unsigned long long *qu
 #ifndef MCK_QLEAD_DIV
 #define MCK_QLEAD_DIV 4
 #endif
-        const uint32_t cl = chunk_log2(n), cu = 1u << cl, lead = cu > MCK_QLEAD_DIV ? cu / MCK_QLEAD_DIV : 1;
-        const uint64_t nch = (n + cu - 1) >> cl;
+        const ChunkPlan plan(n);
+        const uint32_t cl = plan.cl, cu = 1u << cl, lead = cu > MCK_QLEAD_DIV ? cu / MCK_QLEAD_DIV : 1;
+        const uint64_t nch = plan.nch;
 #if MCK_TRACE
         unsigned long long qs_n = 0, qs_sum = 0, qs_max = 0, qs_wait = 0, qs_busy = 0, qs_units = 0;
 #endif
@@ -348,7 +376,9 @@ __device__ __forceinline__ void for_each_unit(WgQueue *L, unsigned long long *qu
             t = __builtin_amdgcn_readfirstlane(t);
             const uint64_t id = uniform64(e) & 0xFFFFFFFFull;
             if (id == kNoChunk) break;
-            const uint64_t u = (id << cl) + (t & (cu - 1));
+            // every chunk spans cu slots; a tail chunk's slots past its size are skipped
+            const uint32_t k = t & (cu - 1);
+            const uint64_t u = k < plan.size(id) ? plan.start(id) + k : n;
 #if MCK_TRACE
             const unsigned long long b0 = wall_clock64();
 #endif

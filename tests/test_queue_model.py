@@ -6,7 +6,8 @@ workgroup leaves the slot's counters at zero for the next launch.
 
 Each wave is a generator that yields at every access to shared state (LDS or
 the global slot), so a seeded scheduler explores many orders of the same
-steps the device code takes.  Fetch triggers, chunk sizes (chunk_log2), the
+steps the device code takes.  Fetch triggers, chunk sizes (chunk_log2, the
+quarter-size tail chunks of ChunkPlan), the
 round-robin sub-queues, the LDS ring recycling and the hierarchical exit
 counting mirror the device code one to one.
 """
@@ -46,7 +47,19 @@ def run_model(n, grid, waves_per_wg, seed, slot=None, max_steps=2_000_000):
     slot = slot or Slot()
     cl = chunk_log2(n, grid)
     cu, lead = 1 << cl, max(1, (1 << cl) // 4) if (1 << cl) > 4 else 1
-    nch = (n + cu - 1) >> cl
+    # ChunkPlan: full chunks, then about one full chunk per workgroup of units
+    # in quarter chunks
+    sl = cl - 2 if cl >= 2 else cl
+    tail = grid << cl
+    nbig = (n - tail) >> cl if n > tail else 0
+    big_end = nbig << cl
+    nch = nbig + ((n - big_end + (1 << sl) - 1) >> sl)
+
+    def start(cid):
+        return cid << cl if cid < nbig else big_end + ((cid - nbig) << sl)
+
+    def size(cid):
+        return 1 << cl if cid < nbig else 1 << sl
     done_units = []
     lds = [Lds() for _ in range(grid)]
 
@@ -92,15 +105,17 @@ def run_model(n, grid, waves_per_wg, seed, slot=None, max_steps=2_000_000):
                 yield from publish(L, seq + 1, nid)
             if e[1] == NOCH:
                 break
-            u = (e[1] << cl) + (t & (cu - 1))
+            k = t & (cu - 1)
+            u = start(e[1]) + k if k < size(e[1]) else n
             if u < n:
                 done_units.append(u)
                 for _ in range(rnd.randint(0, 40)):
                     yield
         # hierarchical exit counting
+        prev_ex = L.exited  # atomicAdd on LDS: the returned old value decides
         L.exited += 1
         yield
-        if L.exited == waves_per_wg:
+        if prev_ex == waves_per_wg - 1:
             g = b % QSUB
             wgs = (grid - g + QSUB - 1) // QSUB
             groups = min(grid, QSUB)
