@@ -317,6 +317,16 @@ def _segment_object_bytes(O, seed, length, j, slots):
                            for q in range(SEGS_PER_OBJECT)])
 
 
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(method, seed, length, offsets_host, got, budget_s, samples, segments=False):
     """The CPU leg (N=1, rank 0): the oracle (CPU restatement of mchecksum --
     the reference's own mchecksum is absent, so kind = "port") timed on this
@@ -332,22 +342,23 @@ def cpu_baseline(method, seed, length, offsets_host, got, budget_s, samples, seg
         slots = segment_slots(seed, len(got) * SEGS_PER_OBJECT)
         n = 256
         host = np.concatenate([_segment_object_bytes(O, seed, length, j, slots) for j in range(n)])
-        run = lambda k: O.batch_fixed(method, host, length, length, k, variant=variant, nthreads=threads)  # noqa: E731
+        runv = lambda k, v, th: O.batch_fixed(method, host, length, length, k, variant=v, nthreads=th)  # noqa: E731
         sample_bytes = n * length
         what = f"the first {n} objects ({SEGS_PER_OBJECT} x {length // SEGS_PER_OBJECT} B segments, gathered)"
     elif offsets_host is None:
         n = 4096 if length <= 65536 else 256
         host = O.splitmix_bytes(n * length, seed)
-        run = lambda k: O.batch_fixed(method, host, length, length, k, variant=variant, nthreads=threads)  # noqa: E731
+        runv = lambda k, v, th: O.batch_fixed(method, host, length, length, k, variant=v, nthreads=th)  # noqa: E731
         sample_bytes = n * length
         what = f"{n} x {length} B"
     else:
         n = int(np.searchsorted(offsets_host, np.uint64(256 << 20)))  # ~256 MiB of whole payloads
         host = O.splitmix_bytes(int(offsets_host[n]), seed)
         sub = np.ascontiguousarray(offsets_host[:n + 1])
-        run = lambda k: O.batch_offsets(method, host, sub[:k + 1], variant=variant, nthreads=threads)  # noqa: E731
+        runv = lambda k, v, th: O.batch_offsets(method, host, sub[:k + 1], variant=v, nthreads=th)  # noqa: E731
         sample_bytes = int(offsets_host[n])
         what = f"the first {n} payloads ({sample_bytes} B) of the offsets layout"
+    run = lambda k: runv(k, variant, threads)  # noqa: E731
     run(64)  # warm
     passes, t0 = 0, time.perf_counter()
     while True:
@@ -359,6 +370,21 @@ def cpu_baseline(method, seed, length, offsets_host, got, budget_s, samples, seg
     base = {"value": round(passes * sample_bytes / el / 2**30, 2), "unit": "GiB/s", "cores": threads, "kind": "port",
             "variant": "x86 SSE4.2 crc32 instruction" if variant == "sse42" else "slicing table",
             "sample": f"{passes} passes over {what} of the same splitmix payloads ({el:.2f} s wall)"}
+    # the other CPU paths on the same sample: 1 thread, and the
+    # table path next to SSE4.2 for CRC-32C
+    legs = [("sse42" if variant == "sse42" else "table", 1)] + ([("table", threads)] if variant == "sse42" else [])
+    breakdown = {}
+    for v, th in legs:
+        p2, t2 = 0, time.perf_counter()
+        while True:
+            runv(n, v, th)
+            p2 += 1
+            e2 = time.perf_counter() - t2
+            if e2 >= budget_s / 3 or p2 >= 50:
+                break
+        breakdown[f"{v}_{th}thread{'s' if th > 1 else ''}"] = round(p2 * sample_bytes / e2 / 2**30, 2)
+    base["breakdown_GiB_s"] = breakdown
+    base["cpu_model"] = _cpu_model()
 
     bad = int(np.count_nonzero(got[:n] != want))
     rng = np.random.default_rng(1234)
