@@ -57,7 +57,9 @@ def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
-    p.add_argument("--warmup", type=int, default=10)
+    # 40: the clock settles after ~30 back-to-back launches (per-launch times
+    # 0.62 -> 0.75 -> 0.62 ms over the first 30, profiles/r01/launch_series_metric.json)
+    p.add_argument("--warmup", type=int, default=40)
     p.add_argument("--config", default="metric", choices=sorted(CONFIGS))
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=1.5, help="wall budget of the CPU baseline sample")

@@ -21,7 +21,7 @@ cd /tmp && export TMPDIR=/tmp
 step "kernel trace"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_metric -o bench -- python3 $R/bench.py > $O/prof_bench.json 2> $O/prof_bench.err || { tail $O/prof_bench.err; exit 1; }
 for c in ${PMC_CONFIGS:-metric c2 c3 c4 seg}; do
-  k=crc32c_batch_kernel; n=1; [ $c = c3 ] && k=crc64_batch_kernel; [ $c = seg ] && { k=seg_; n=3; }
+  k=crc32c_batch_kernel; n=1; [ $c = c3 ] && k=crc64_batch_kernel; [ $c = seg ] && { k=seg_; n=5; }
   step "pmc fetch/write $c"
   timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch_$c -o pmc -- python3 $R/bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline > $O/pmc_fetch_$c.json 2> $O/pmc_fetch_$c.err || { tail $O/pmc_fetch_$c.err; exit 1; }
   timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write_$c -o pmc -- python3 $R/bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline > $O/pmc_write_$c.json 2> $O/pmc_write_$c.err || { tail $O/pmc_write_$c.err; exit 1; }
