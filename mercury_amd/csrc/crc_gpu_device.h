@@ -128,18 +128,21 @@ struct BatchArgs {
 // work: device-scope atomics on one address retire ~1 per 45 ns on MI355X,
 // so 8 per-XCD counters fed one ticket per payload group throttled C2 2.6x.
 //
-// Two levels instead.  Units [0, n) form chunks of 2^cl units; the chunk
+// Two levels instead.  Units [0, n) form chunks (ChunkPlan below); the chunk
 // ids are dealt round-robin to 8 sub-queues (one per XCD by blockIdx % 8, the
-// dispatch order), each a global counter on its own 256-B line.  A
-// workgroup takes whole chunks (one global atomic per 16 units, stealing from
-// the next sub-queue once its own is drained) and its waves take the chunk's
-// units one at a time through an LDS counter.  The wave that takes a chunk's
-// first slot fetches the NEXT chunk, so a fetch's latency hides under a whole
-// chunk of scanning; chunk ids pass through a small LDS ring whose entries
-// are recycled only after all 2^cl readers of the previous occupant have
-// read it.  The last wave of the grid zeroes the global counters, leaving the
-// slot ready for the next launch (the host hands each launch a slot from a
-// ring, mchecksum_gpu.hip).
+// dispatch order), each a global counter on its own 256-B line.  A workgroup
+// takes whole chunks (one device-scope atomic per chunk, stealing from the
+// next sub-queue once its own is drained) and its waves take the chunk's
+// units one at a time through an LDS counter.  The wave that takes the slot a
+// quarter chunk before the end fetches the NEXT chunk -- after reading its own
+// chunk id, so fetches run in chunk order and the first "no more chunks" is
+// final -- and the fetch's latency hides under the rest of the chunk.  Chunk
+// ids pass through a small LDS ring whose entries are recycled only after all
+// readers of the previous occupant have read it.  Exit counting is
+// hierarchical (LDS per workgroup, one line per group, one per slot) and the
+// last group zeroes the slot for the next launch (the host hands each launch
+// a slot from a ring, mchecksum_gpu.hip).  tests/test_queue_model.py runs the
+// same protocol on the CPU under random interleavings.
 // Slot layout (one counter per 256-B line): [0, 8) sub-queue tickets,
 // [8, 16) exited workgroups per group (blockIdx % 8), [16] exited groups.
 constexpr uint32_t kQSub = 8;
