@@ -113,3 +113,34 @@ def test_queue_slot_survives_graph_replay(gpu, oracle_mod, monkeypatch):
         assert np.array_equal(G.as_unsigned(out_o).astype(np.uint64), want_o)
         assert np.array_equal(G.as_unsigned(out_f).astype(np.uint64), want_f)
     assert G.queue_faults() == 0
+
+
+def test_concurrent_streams_get_distinct_slots(gpu, oracle_mod, monkeypatch):
+    """Queue-driven launches on four streams at once (each takes its own slot
+    from the ring) all return the oracle's values."""
+    import torch
+    G, O = gpu, oracle_mod
+    monkeypatch.setenv("MCHECKSUM_GPU_LIGHT", "0")
+    host = O.splitmix_bytes(16 << 20, 5151)
+    dev = torch.cat([torch.from_numpy(host).cuda(), torch.zeros(64, dtype=torch.uint8, device="cuda")])
+    rng = np.random.default_rng(3)
+    tables, outs, wants = [], [], []
+    for k in range(4):
+        offs = np.zeros(4001, dtype=np.uint64)
+        offs[1:] = np.cumsum(rng.integers(0, 4000, 4000))
+        offs += np.uint64(k * 997)
+        tables.append((offs, torch.from_numpy(offs.astype(np.int64)).cuda()))
+        wants.append(O.batch_offsets("crc64" if k % 2 else "crc32c", host, offs, nthreads=8))
+    G.prepare("crc32c")
+    G.prepare("crc64")
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream() for _ in range(4)]
+    for rep in range(3):
+        for k, s in enumerate(streams):
+            with torch.cuda.stream(s):
+                outs.append(G.checksum_offsets("crc64" if k % 2 else "crc32c", dev, tables[k][1], stream=s))
+        _wait(torch, "concurrent streams")
+        torch.cuda.synchronize()
+    for i, o in enumerate(outs):
+        assert np.array_equal(G.as_unsigned(o).astype(np.uint64), wants[i % 4]), i
+    assert G.queue_faults() == 0
