@@ -30,6 +30,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 #include <mutex>
 
 #include "crc_gpu_device.h"
@@ -327,12 +328,19 @@ using namespace mck;
 extern "C" {
 
 int mchecksum_gpu_available(void) {
+    // The device count cannot change for the life of the process: ask HIP
+    // once (every batch call checks this first; ~1 us saved per call).
+    static std::atomic<int> cached{-1};
+    int v = cached.load(std::memory_order_relaxed);
+    if (v >= 0) return v;
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) {
         (void)hipGetLastError();
-        return 0;
+        n = 0;
     }
-    return n > 0 ? 1 : 0;
+    v = n > 0 ? 1 : 0;
+    cached.store(v, std::memory_order_relaxed);
+    return v;
 }
 
 int mchecksum_gpu_prepare(const char *hash_method) {

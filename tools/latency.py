@@ -33,8 +33,17 @@ def main():
           t0 = time.perf_counter()
           for _ in range(n):
               f()
+          issue_us = (time.perf_counter() - t0) / n * 1e6  # host cost of one call (queue not full)
           torch.cuda.synchronize()
           eager_us = (time.perf_counter() - t0) / n * 1e6
+          # the C-ABI call alone (no torch wrapper): host cost of the entry point
+          L = G._lib()
+          h = torch.cuda.current_stream().cuda_stream
+          t1 = time.perf_counter()
+          for _ in range(n):
+              L.mchecksum_gpu_checksum_fixed(b"crc32c", big.data_ptr(), length, length, count, out.data_ptr(), h)
+          capi_us = (time.perf_counter() - t1) / n * 1e6
+          torch.cuda.synchronize()
           g = torch.cuda.CUDAGraph()
           with torch.cuda.graph(g):
               f()
@@ -47,7 +56,7 @@ def main():
           torch.cuda.synchronize()
           graph_us = (time.perf_counter() - t0) / n * 1e6
           r = {"light": light, "payloads": count, "bytes": count * length, "device_us": round(dev_us, 2),
-               "eager_wall_us_per_call": round(eager_us, 2), "graph_wall_us_per_replay": round(graph_us, 2),
+               "eager_wall_us_per_call": round(eager_us, 2), "host_issue_us": round(issue_us, 2), "capi_issue_us": round(capi_us, 2), "graph_wall_us_per_replay": round(graph_us, 2),
                "graph_result_identical": same, "GBps_device": round(count * length / dev_us / 1e3, 1)}
           print(json.dumps(r), flush=True)
           res.append(r)
