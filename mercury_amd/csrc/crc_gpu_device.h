@@ -54,7 +54,8 @@ struct Tab32 {
 };
 // CRC-64 LDS map.  A 64-bit state is looked up by nibble: the 8 low-nibble
 // tables are replicated 32x (entry v at v*256 B, lane copy at (lane%32)*8 B;
-// the address is one v_perm of the masked nibble and the lane byte), the 8
+// the address is one v_and_b32_sdwa of the nibble into the lane-copy register,
+// f64x_byte below), the 8
 // high-nibble tables are NOT replicated: entry v sits at v*16 B, so the masked
 // byte (v << 4) is its own address and the 16 entries fall on 16 distinct bank
 // pairs of ds_read_b64 (lanes that share an entry broadcast) -- conflict-free
@@ -116,7 +117,7 @@ struct BatchArgs {
     // message mode (verify_messages): payload i = [offsets[i] + pay_off,
     // offsets[i+1]), expected CRC = big-endian u32 at offsets[i] + hash_off
     uint32_t msg, pay_off, hash_off;
-    // work-queue slot (WorkQueue below); nullptr = static assignment
+    // work-queue slot (WgQueue below); nullptr = static assignment
     unsigned long long *queue;
 };
 

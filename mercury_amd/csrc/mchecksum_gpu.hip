@@ -14,15 +14,21 @@
 //    uniform stride of 16*G bytes, so "advance by the stride" is folded into
 //    the lookup tables: s <- F(s ^ w) costs 4 byte lookups (CRC-32C) or 16
 //    nibble lookups (CRC-64) and no shift/multiply.
-//  * Lookup tables live in LDS, replicated 32x so lane l always hits bank
-//    l % 32: every ds_read_b32/b64 is conflict-free.  Addresses are formed by
-//    one v_perm_b32 per lookup (byte -> entry stride 256 B, lane copy in the
-//    low byte).
+//  * Lookup tables live in LDS, laid out so that every ds_read_b32/b64 is
+//    conflict-free: CRC-32C byte tables and CRC-64 low-nibble tables are
+//    replicated 32x (lane l reads copy l % 32), CRC-64 high-nibble tables sit
+//    at a 16-B entry stride.  One VALU op forms each lookup address (v_perm_b32
+//    or v_and_b32_sdwa: the byte or nibble as entry, the lane copy in the low
+//    byte).
 //  * Sub-streams are combined by a tree (in-lane, then xor-shuffles across the
 //    group) whose level operators Z^-(2^k * W/8) are nibble tables in LDS;
 //    Z^-t removes the t pad bytes after the payload end.
-//  * One 1024-thread workgroup per CU (the replicated tables take 128 KiB of
-//    the 160 KiB LDS), persistent over the batch: waves stride over payloads.
+//  * Persistent grid: one 1024-thread workgroup per CU for CRC-32C (the
+//    replicated tables take 128 KiB of the 160 KiB LDS), two for CRC-64.  Waves
+//    take payloads from a device-side work queue (large aligned CRC-32C and
+//    all offsets batches) or by a static stride (crc_gpu_device.h, dyn_policy).
+//    Batches <= 16 MiB take a light layout: unreplicated tables, 256-thread
+//    workgroups on every CU.
 // No MFMA: this is HBM-bound byte scanning; the roofline is HBM read bandwidth.
 #include <hip/hip_runtime.h>
 
@@ -246,7 +252,6 @@ int prologue(const char *method, int log2g, int *width, DevCtx **c, const void *
     return get_pack(*c, idx, log2g, pack);
 }
 
-// The work queue's chunk ids are 32-bit (crc_gpu_device.h, WgQueue).
 // The work queue counts chunk ids and per-workgroup slots in 32 bits
 // (crc_gpu_device.h, WgQueue): 2^31 payloads per call keeps both in range.
 constexpr uint64_t kMaxUnits = 1ull << 31;
@@ -366,6 +371,9 @@ int mchecksum_gpu_checksum_fixed(const char *hash_method, const void *dev_base, 
     if (count && (!dev_base || !dev_out)) return set_err(MCHECKSUM_GPU_EINVAL, "NULL pointer argument");
     if (count > 1 && stride < len) return set_err(MCHECKSUM_GPU_EINVAL, "stride smaller than len");
     if ((uint64_t)count > kMaxUnits) return set_err(MCHECKSUM_GPU_EINVAL, "more than 2^31 payloads in one call");
+    // the batch must fit the address space: stride * (count - 1) + len
+    if (count > 1 && (uint64_t)stride > (UINT64_MAX - (uint64_t)len) / (count - 1))
+        return set_err(MCHECKSUM_GPU_EINVAL, "stride * (count - 1) + len overflows");
     if (!mchecksum_gpu_available()) return set_err(MCHECKSUM_GPU_ENODEV, "no HIP device");
     int width = 0;
     if (gpu_model(hash_method, &width) >= 0 && width == 32 && use_light((uint64_t)len * count, true)) {

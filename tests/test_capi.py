@@ -71,6 +71,30 @@ def test_no_gpu_means_loud_failure_not_fallback(product_lib):
     assert b"device" in L.mchecksum_gpu_last_error()
 
 
+def test_batch_arguments_rejected_before_any_device_work(product_lib):
+    """Bad batch arguments give MCHECKSUM_GPU_EINVAL (-1) and a reason,
+    whether or not a device is present (checked before device detection)."""
+    L = product_lib
+    buf = ctypes.create_string_buffer(64)
+    offs = (ctypes.c_uint64 * 2)(0, 64)
+    cases = [
+        (lambda: L.mchecksum_gpu_checksum_fixed(b"crc32c", None, 64, 64, 1, buf, None), "NULL"),
+        (lambda: L.mchecksum_gpu_checksum_fixed(b"crc32c", buf, 64, 64, 1, None, None), "NULL"),
+        (lambda: L.mchecksum_gpu_checksum_fixed(b"crc32c", buf, 32, 64, 2, buf, None), "stride"),
+        (lambda: L.mchecksum_gpu_checksum_fixed(b"crc32c", buf, 64, 64, (1 << 31) + 1, buf, None), "2^31"),
+        (lambda: L.mchecksum_gpu_checksum_fixed(b"crc32c", buf, 1 << 62, 64, 8, buf, None), "overflows"),
+        (lambda: L.mchecksum_gpu_checksum_offsets(b"crc32c", buf, None, 1, buf, None), "NULL"),
+        (lambda: L.mchecksum_gpu_checksum_offsets(b"crc32c", buf, offs, (1 << 31) + 1, buf, None), "2^31"),
+        (lambda: L.mchecksum_gpu_verify_offsets(b"crc32c", buf, offs, 1, None, None, None, None), "NULL"),
+        (lambda: L.mchecksum_gpu_verify_messages(b"crc32c", buf, offs, 1, 18, 16, None, None, None), "hash_offset"),
+    ]
+    for call, why in cases:
+        assert call() == -1, why
+        assert why.encode() in L.mchecksum_gpu_last_error(), (why, L.mchecksum_gpu_last_error())
+    # an empty batch is valid with NULL buffers
+    assert L.mchecksum_gpu_checksum_fixed(b"crc32c", None, 0, 0, 0, None, None) in (0, -2)
+
+
 def test_lanes_per_payload_heuristic(product_lib):
     f = product_lib.mchecksum_gpu_lanes_per_payload
     assert f(b"crc32c", 65536) == 64
