@@ -110,7 +110,8 @@ mchecksum_gpu_verify_messages(const char *hash_method, const void *dev_buf,
  * dev_obj_first holds nobj + 1 non-decreasing indices <= nseg; segments
  * outside [first[0], first[nobj]) are ignored.  dev_work: caller-owned device
  * scratch (8-byte aligned) of at least mchecksum_gpu_segments_work_size(nseg)
- * bytes, not shared with a concurrent call.  crc32c and crc64.  Segments are
+ * bytes, not shared with a concurrent call (SIZE_MAX for nseg > 2^40, which
+ * is rejected).  crc32c and crc64.  Segments are
  * cut into 256 KiB chunks hashed in parallel and recombined with GF(2) shift
  * operators, so one huge segment still spreads over the whole GPU. */
 MCHECKSUM_PUBLIC size_t

@@ -495,7 +495,11 @@ using namespace mck;
 extern "C" {
 
 // P, C (nseg + 1 each), the ragged flag (+ pad), 3 words per scan block.
+// More than 2^40 segments (far beyond device memory) is rejected, so the size
+// cannot wrap: SIZE_MAX then makes any allocation of it fail.
+constexpr uint64_t kMaxSegs = 1ull << 40;
 size_t mchecksum_gpu_segments_work_size(size_t nseg) {
+    if ((uint64_t)nseg > kMaxSegs) return SIZE_MAX;
     return sizeof(uint64_t) * (2 * (nseg + 1) + 2 + 3 * ((nseg + kScanBlk - 1) / kScanBlk));
 }
 
@@ -504,6 +508,7 @@ int mchecksum_gpu_checksum_segments(const char *hash_method, const uint64_t *dev
                                     size_t nobj, void *dev_work, size_t work_size, void *dev_out, void *stream) {
     if (!dev_obj_first || (nobj && !dev_out) || (nseg && (!dev_seg_addr || !dev_seg_len)) || !dev_work)
         return set_err(MCHECKSUM_GPU_EINVAL, "NULL pointer argument");
+    if ((uint64_t)nseg > kMaxSegs) return set_err(MCHECKSUM_GPU_EINVAL, "more than 2^40 segments in one call");
     if (work_size < mchecksum_gpu_segments_work_size(nseg) || (uintptr_t)dev_work % 8)
         return set_err(MCHECKSUM_GPU_EINVAL, "workspace smaller than mchecksum_gpu_segments_work_size() or unaligned");
     if (!mchecksum_gpu_available()) return set_err(MCHECKSUM_GPU_ENODEV, "no HIP device");

@@ -88,6 +88,16 @@ def test_batch_arguments_rejected_before_any_device_work(product_lib):
         (lambda: L.mchecksum_gpu_verify_offsets(b"crc32c", buf, offs, 1, None, None, None, None), "NULL"),
         (lambda: L.mchecksum_gpu_verify_messages(b"crc32c", buf, offs, 1, 18, 16, None, None, None), "hash_offset"),
     ]
+    ws = L.mchecksum_gpu_segments_work_size
+    ws.restype = ctypes.c_size_t
+    assert ws(4) == 8 * (2 * 5 + 2 + 3) and ws((1 << 40) + 1) == (1 << 64) - 1
+    first = (ctypes.c_uint64 * 2)(0, 1)
+    cases += [
+        (lambda: L.mchecksum_gpu_checksum_segments(b"crc64", offs, offs, 1, first, 1, buf, 8, buf, None), "workspace"),
+        (lambda: L.mchecksum_gpu_checksum_segments(b"crc64", offs, offs, (1 << 40) + 1, first, 1, buf, 64, buf, None),
+         "2^40"),
+        (lambda: L.mchecksum_gpu_verify_core_headers(b"crc16", 7, buf, offs, 1, None, None, None), "kind"),
+    ]
     for call, why in cases:
         assert call() == -1, why
         assert why.encode() in L.mchecksum_gpu_last_error(), (why, L.mchecksum_gpu_last_error())
