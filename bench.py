@@ -61,6 +61,9 @@ def parse():
     # 0.62 -> 0.75 -> 0.62 ms over the first 30, profiles/r01/launch_series_metric.json)
     p.add_argument("--warmup", type=int, default=40)
     p.add_argument("--config", default="metric", choices=sorted(CONFIGS))
+    p.add_argument("--streams", type=int, default=1,
+                   help="issue consecutive steps round-robin on this many streams (independent batches, "
+                        "fixed and offsets layouts)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=1.5, help="wall budget of the CPU baseline sample")
     p.add_argument("--parity-samples", type=int, default=64)
@@ -154,10 +157,20 @@ def main():
         G.checksum_offsets(method, data, offsets_dev, offsets_host=offsets_host)  # validates the table once
         run = lambda out: G.checksum_offsets(method, data, offsets_dev, out=out)  # noqa: E731
     out = torch.empty(count, dtype=G.out_dtype(method), device=dev)
+    if args.streams > 1 and layout not in ("fixed", "offsets"):
+        raise SystemExit(f"--streams > 1 needs a fixed or offsets layout (config {args.config} shares scratch)")
+    streams = [stream] + [torch.cuda.Stream(device=dev) for _ in range(args.streams - 1)]
+    outs = [out] + [torch.empty_like(out) for _ in range(args.streams - 1)]
     torch.cuda.synchronize()
 
-    for _ in range(args.warmup):
-        run(out)
+    def step(i):  # step i: one batch, on stream i % S with its own output
+        s = streams[i % len(streams)]
+        with torch.cuda.stream(s):
+            run(outs[i % len(streams)])
+        return s
+
+    for i in range(args.warmup):
+        step(i)
     torch.cuda.synchronize()
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
@@ -166,9 +179,10 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        ev[i][0].record(stream)
-        run(out)
-        ev[i][1].record(stream)
+        s = streams[i % len(streams)]
+        ev[i][0].record(s)
+        step(i)
+        ev[i][1].record(s)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
