@@ -1,3 +1,5 @@
+#!/bin/bash
+# bench.py for metric and c4 with 1, 2 and 3 streams (independent batches round-robin).
 set -o pipefail
 cd ${GRAFT_REPO_ROOT:-/root/repo}; mkdir -p gpurun_out
 for c in metric c4; do for s in 1 2 1 2 3; do
