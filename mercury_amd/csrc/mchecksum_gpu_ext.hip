@@ -295,6 +295,8 @@ __device__ __forceinline__ void seg_object_terms(const SegArgs &a) {
 template <int KEY>
 constexpr int kSegWavesPerEU = KEY == 64 * 4 + 1 ? 8 : 1;
 
+constexpr uint64_t kSegNtBytes = 512ull << 20;
+
 template <int W, int PART>
 __global__ __launch_bounds__(1024, kSegWavesPerEU<W * 4 + PART>) void seg_kernel(SegArgs a) {
     if (PART == 2 && *a.ragged == 0) {  // every chunk took the aligned pass: object terms only
@@ -315,6 +317,7 @@ __global__ __launch_bounds__(1024, kSegWavesPerEU<W * 4 + PART>) void seg_kernel
         const Tab32<false> lds{lds_raw};
         const uint32_t lc0 = (lane & 31u) << 2, lc1 = lc0 | 0x10000u;
         uint32_t *out = reinterpret_cast<uint32_t *>(a.out);
+        const bool nt = uniform(a.P[a.nseg]) >= kSegNtBytes;  // as for CRC-64 below
         ChunkWalk walk(a, wave, nw, nchunks);
         uint64_t p, n, j, after;
         bool in;
@@ -323,9 +326,10 @@ __global__ __launch_bounds__(1024, kSegWavesPerEU<W * 4 + PART>) void seg_kernel
             const uint8_t *q = reinterpret_cast<const uint8_t *>(p);
             // whole 1 KiB steps from a 16-B aligned start (the usual bulk
             // segment) take the aligned loop: no edge masks, no pad operator
-            uint32_t x = p % 16 == 0 && n % 1024 == 0
-                             ? payload32_aligned<6, false>(lds, q, n >> 10, lane, lc0, lc1, 0u)
-                             : payload32_g64<false, Tab32<false>, true>(lds, pk, q, n, lane, lc0, lc1);
+            const bool aligned = p % 16 == 0 && n % 1024 == 0;
+            uint32_t x = aligned && nt    ? payload32_aligned<6, true>(lds, q, n >> 10, lane, lc0, lc1, 0u)
+                         : aligned        ? payload32_aligned<6, false>(lds, q, n >> 10, lane, lc0, lc1, 0u)
+                                          : payload32_g64<false, Tab32<false>, true>(lds, pk, q, n, lane, lc0, lc1);
             x = shift32(sp, uniform(x), after);
             if (lane == 0) atomicXor(out + j, x);
         }
@@ -338,6 +342,12 @@ __global__ __launch_bounds__(1024, kSegWavesPerEU<W * 4 + PART>) void seg_kernel
         __syncthreads();
         const uint32_t lc = (lane & 31u) << 3;
         unsigned long long *out = reinterpret_cast<unsigned long long *>(a.out);
+        // Non-temporal payload loads once the batch is far larger than the
+        // Infinity Cache, as for fixed batches.  Here the size is only known on
+        // the device (the segment scan's total), so the choice is a uniform
+        // branch per chunk: +3% on `seg` (duplicating the whole walk under one
+        // branch measured the same and spills more).
+        [[maybe_unused]] const bool nt = uniform(a.P[a.nseg]) >= kSegNtBytes;
         ChunkWalk walk(a, wave, nw, nchunks);
         uint64_t p, n, j, after;
         bool in;
@@ -348,7 +358,8 @@ __global__ __launch_bounds__(1024, kSegWavesPerEU<W * 4 + PART>) void seg_kernel
             if (aligned != (PART == 1)) continue;
             uint64_t x;
             if constexpr (PART == 1)
-                x = payload64_aligned<6, false, false>(lds, pk, q, (uint32_t)(n >> 10), lane, lc, 0ull);
+                x = nt ? payload64_aligned<6, true, false>(lds, pk, q, (uint32_t)(n >> 10), lane, lc, 0ull)
+                       : payload64_aligned<6, false, false>(lds, pk, q, (uint32_t)(n >> 10), lane, lc, 0ull);
             else
                 x = payload64_g64<false, true>(lds, pk, q, n, lane, lc);
             x = shift64(sp, uniform(x), after);

@@ -211,3 +211,19 @@ def test_segments_long_lists_multi_block_scan(gpu, buf, oracle_mod, method):
     first = list(range(0, 3001, 3))
     got = gpu.as_unsigned(gpu.checksum_segments(method, [buf[o:o + n] for o, n in segs], first))
     assert got.tolist() == _want(oracle_mod, method, host, segs, first)
+
+
+@pytest.mark.parametrize("method", ["crc32c", "crc64"])
+def test_segments_large_batch_non_temporal(gpu, buf, oracle_mod, method):
+    """>= 512 MiB in one call takes the non-temporal loads (decided on the
+    device from the scan's total): 640 segments of 1 MiB, views that reuse the
+    24 MiB buffer at 16-B aligned offsets, 4 per object, plus a few ragged ones."""
+    rng = np.random.default_rng(91 if method == "crc32c" else 92)
+    host = _host(buf)
+    mib = 1 << 20
+    segs = [(16 * int(rng.integers(0, (buf.numel() - 64 - mib) // 16)), mib) for _ in range(640)]
+    segs[5] = (segs[5][0] + 3, mib - 7)  # ragged: takes the generic pass
+    first = list(range(0, 641, 4))
+    got = gpu.as_unsigned(gpu.checksum_segments(method, [buf[o:o + n] for o, n in segs], first)).tolist()
+    for j in (0, 1, 17, 80, 159):
+        assert got[j] == _want(oracle_mod, method, host, segs[first[j]:first[j + 1]], [0, 4])[0], j
