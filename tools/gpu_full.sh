@@ -20,6 +20,7 @@ done
 cd /tmp && export TMPDIR=/tmp
 step "kernel trace"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_metric -o bench -- python3 $R/bench.py > $O/prof_bench.json 2> $O/prof_bench.err || { tail $O/prof_bench.err; exit 1; }
+python3 $R/tools/trace_steady.py $O/prof_metric/bench_kernel_trace.csv crc32c_batch_kernel 40 50 $O/prof_bench.json > $O/metric_kernel_steady.json && cat $O/metric_kernel_steady.json
 for c in ${PMC_CONFIGS:-metric c2 c3 c4 seg}; do
   k=crc32c_batch_kernel; n=1; [ $c = c3 ] && k=crc64_batch_kernel; [ $c = seg ] && { k=seg_; n=5; }
   step "pmc fetch/write $c"
