@@ -2,9 +2,10 @@
 
 Every case runs through the C ABI (libmchecksum.so, via mercury_amd.gpu) on
 device-resident bytes and compares with oracle/ on the same bytes.  Sizes the
-oracle finishes in seconds are compared exhaustively; the full BASELINE
-shapes are compared on sampled payloads plus size-independent properties
-(determinism, single-bit corruption detected exactly where injected).
+oracle finishes in seconds are compared exhaustively; here the full BASELINE
+shapes add size-independent properties (determinism, single-bit corruption
+detected exactly where injected), and test_gpu_full_shapes.py checks every
+payload of them against the oracle.
 """
 import os
 
