@@ -1,9 +1,10 @@
 """Batch checksums of device-resident payloads on MI355X (include/mchecksum_gpu.h).
 
 Thin torch-facing wrappers over the C ABI: torch only provides device memory
-and streams here.  Every function checks shapes on the host before the
-kernel launch (so a bad argument can never turn into an out-of-bounds read on
-the GPU) and raises on any error -- there is no CPU fallback.
+and streams here.  Every function checks tensor shapes, dtypes and bounds on
+the host before the kernel launch and raises on any error -- there is no CPU
+fallback.  Offsets tables live on the device: they are bounds-checked when a
+host copy is passed (offsets_host=...), otherwise trusted, as in the C ABI.
 """
 from __future__ import annotations
 
@@ -122,6 +123,8 @@ def checksum_offsets(method: str, data: torch.Tensor, offsets: torch.Tensor, out
         raise GpuChecksumError("offsets needs at least one entry")
     if out is None:
         out = torch.empty(count, dtype=out_dtype(method), device=data.device)
+    elif out.numel() < count or out.dtype != out_dtype(method) or not out.is_cuda:
+        raise GpuChecksumError("out tensor has the wrong size, dtype or device")
     rc = _lib().mchecksum_gpu_checksum_offsets(method.encode(), data.data_ptr(), offsets.data_ptr(), count,
                                                out.data_ptr(), _stream_handle(stream))
     if rc != 0:
