@@ -21,15 +21,20 @@ struct DevCtx {
     int cus = 0;
     void *pack[MCK_NMODELS][CRC_GPU_MAX_LOG2G + 1] = {};
     void *ext[MCK_NMODELS] = {};  // mchecksum_gpu_ext.hip's per-model tables
-    // Work-queue slots of the batch kernels (WorkQueue, crc_gpu_device.h): a
-    // ring of kQueueSlots zeroed counter sets; each launch takes the next slot
-    // and its last wave re-zeroes it.  Launches that run at the same time
-    // (different streams) get different slots unless more than kQueueSlots
-    // are in flight at once.
+    // Work-queue slots of the batch kernels (WgQueue, crc_gpu_device.h):
+    // kQueueSlots zeroed counter sets; a launch's last wave re-zeroes its slot.
+    // Eager launches take the next slot of a ring of kEagerSlots, so launches
+    // that run at the same time (different streams) get different slots unless
+    // more than kEagerSlots are in flight at once.  A launch captured into a
+    // hipGraph keeps its slot for every replay, so it gets one of its own from
+    // the remaining kCapturedSlots, never handed out again.
     unsigned long long *queue = nullptr;
     uint32_t queue_next = 0;
+    uint32_t queue_captured = 0;
 };
 constexpr uint32_t kQueueSlots = 4096;
+constexpr uint32_t kCapturedSlots = 1024;
+constexpr uint32_t kEagerSlots = kQueueSlots - kCapturedSlots;
 
 extern std::mutex g_mu;
 
@@ -42,8 +47,9 @@ int gpu_model(const char *method, int *width);
 int device_ctx(DevCtx **out);
 // Model + device context + table pack for lanes-per-payload 2^log2g (takes g_mu).
 int prologue(const char *method, int log2g, int *width, DevCtx **c, const void **pack);
-// Work-queue slot for one launch of a throughput (non-light) batch kernel.
-unsigned long long *queue_slot(DevCtx *c);
+// Work-queue slot for one launch of a throughput (non-light) batch kernel on
+// `stream`; nullptr (error recorded) once a device's captured slots run out.
+unsigned long long *queue_slot(DevCtx *c, void *stream);
 
 }  // namespace mck
 

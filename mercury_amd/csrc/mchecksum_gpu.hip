@@ -141,8 +141,21 @@ int get_pack(DevCtx *c, int idx, int log2g, const void **pack) {
     return 0;
 }
 
-unsigned long long *queue_slot(DevCtx *c) {
-    const uint32_t s = __atomic_fetch_add(&c->queue_next, 1u, __ATOMIC_RELAXED) % kQueueSlots;
+unsigned long long *queue_slot(DevCtx *c, void *stream) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing((hipStream_t)stream, &st) != hipSuccess) {
+        (void)hipGetLastError();
+        st = hipStreamCaptureStatusNone;
+    }
+    if (st == hipStreamCaptureStatusActive) {
+        const uint32_t k = __atomic_fetch_add(&c->queue_captured, 1u, __ATOMIC_RELAXED);
+        if (k >= kCapturedSlots) {
+            set_err(MCHECKSUM_GPU_EINVAL, "more than %u graph-captured queue launches on this device", kCapturedSlots);
+            return nullptr;
+        }
+        return c->queue + (size_t)(kEagerSlots + k) * kQSlotWords;
+    }
+    const uint32_t s = __atomic_fetch_add(&c->queue_next, 1u, __ATOMIC_RELAXED) % kEagerSlots;
     return c->queue + (size_t)s * kQSlotWords;
 }
 
@@ -301,7 +314,7 @@ int do_offsets(const char *method, const void *base, const uint64_t *offsets, si
     else
         k = verify ? (nt ? kernel_ptr<64, 6, kOffsets, true, true>() : kernel_ptr<64, 6, kOffsets, true>())
                    : (nt ? kernel_ptr<64, 6, kOffsets, false, true>() : kernel_ptr<64, 6, kOffsets, false>());
-    if (dyn_policy(width, kOffsets, nt, light)) a.queue = queue_slot(c);
+    if (dyn_policy(width, kOffsets, nt, light) && !(a.queue = queue_slot(c, stream))) return MCHECKSUM_GPU_EINVAL;
     return launch(k, a, grid_for(c, count, k), stream);
 }
 
@@ -322,7 +335,8 @@ int launch_fixed(DevCtx *c, const void *pack, int width, int lg, const void *dev
     const bool nt = !light && use_nt((uint64_t)len * count);
     const KLaunch k = width == 32 ? pick_fixed<32>(lg, aligned, nt, light) : pick_fixed<64>(lg, aligned, nt, false);
     const uint64_t ppw = 64u >> lg;
-    a.queue = dyn_policy(width, aligned ? kFixedAligned : kFixedGeneric, nt, light) ? queue_slot(c) : nullptr;
+    if (dyn_policy(width, aligned ? kFixedAligned : kFixedGeneric, nt, light) && !(a.queue = queue_slot(c, stream)))
+        return MCHECKSUM_GPU_EINVAL;
     return launch(k, a, grid_for(c, (count + ppw - 1) / ppw, k), stream);
 }
 

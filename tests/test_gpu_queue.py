@@ -13,11 +13,14 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _wait(torch, tag):
-    ev = torch.cuda.Event()
-    ev.record()
+def _wait(torch, tag, streams=(None,)):
+    evs = []
+    for st in streams:
+        ev = torch.cuda.Event()
+        ev.record(st)
+        evs.append(ev)
     t0 = time.time()
-    while not ev.query():
+    while not all(ev.query() for ev in evs):
         if time.time() - t0 > 20:
             print("HUNG", tag, flush=True)
             os._exit(3)
@@ -139,8 +142,51 @@ def test_concurrent_streams_get_distinct_slots(gpu, oracle_mod, monkeypatch):
         for k, s in enumerate(streams):
             with torch.cuda.stream(s):
                 outs.append(G.checksum_offsets("crc64" if k % 2 else "crc32c", dev, tables[k][1], stream=s))
-        _wait(torch, "concurrent streams")
+        _wait(torch, "concurrent streams", streams)
         torch.cuda.synchronize()
     for i, o in enumerate(outs):
         assert np.array_equal(G.as_unsigned(o).astype(np.uint64), wants[i % 4]), i
     assert G.queue_faults() == 0
+
+
+def test_graph_slot_is_never_reused_by_eager_launches(gpu, oracle_mod, monkeypatch):
+    """A captured launch owns its queue slot: 4300 eager launches on another
+    stream wrap the eager ring more than once while the graph keeps replaying
+    concurrently, and neither side loses or repeats a unit."""
+    import torch
+    G, O = gpu, oracle_mod
+    monkeypatch.setenv("MCHECKSUM_GPU_LIGHT", "0")
+    host = O.splitmix_bytes(8 << 20, 777)
+    dev = torch.cat([torch.from_numpy(host).cuda(), torch.zeros(64, dtype=torch.uint8, device="cuda")])
+    rng = np.random.default_rng(21)
+    tabs = []
+    for _ in range(2):
+        offs = np.zeros(2049, dtype=np.uint64)
+        offs[1:] = np.cumsum(rng.integers(0, 2048, 2048))
+        tabs.append((offs, torch.from_numpy(offs.astype(np.int64)).cuda()))
+    want_g = O.batch_offsets("crc32c", host, tabs[0][0], nthreads=8)
+    want_e = O.batch_offsets("crc32c", host, tabs[1][0], nthreads=8)
+    G.prepare("crc32c")
+    out_g = torch.zeros(2048, dtype=torch.int32, device="cuda")
+    outs_e = [torch.zeros(2048, dtype=torch.int32, device="cuda") for _ in range(2)]
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Stream(), torch.cuda.Stream()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s), torch.cuda.graph(g, stream=s):
+        G.checksum_offsets("crc32c", dev, tabs[0][1], out=out_g)
+    torch.cuda.synchronize()
+    bad = 0
+    for i in range(4300):
+        with torch.cuda.stream(e):
+            G.checksum_offsets("crc32c", dev, tabs[1][1], out=outs_e[i % 2], stream=e)
+        if i % 100 == 0:
+            with torch.cuda.stream(s):
+                g.replay()
+        if i % 500 == 499:
+            _wait(torch, ("eager", i), (s, e))
+            torch.cuda.synchronize()
+            bad += int(not np.array_equal(G.as_unsigned(out_g).astype(np.uint64), want_g))
+            bad += sum(int(not np.array_equal(G.as_unsigned(o).astype(np.uint64), want_e)) for o in outs_e)
+    _wait(torch, "final", (s, e))
+    torch.cuda.synchronize()
+    assert bad == 0 and G.queue_faults() == 0
