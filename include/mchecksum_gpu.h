@@ -24,7 +24,9 @@
  *
  * Streams: `stream` is a hipStream_t (NULL = the default stream).  Calls are
  * asynchronous and capture-safe once mchecksum_gpu_prepare() has run for the
- * method on the current device (it uploads the lookup tables).
+ * method on the current device (it uploads the lookup tables).  Up to 3072
+ * calls may be in flight at once per device; each captured call keeps a
+ * device-side work-queue slot of its own for every replay, 1024 per device.
  *
  * There is NO host fallback: without a usable HIP device every call returns
  * MCHECKSUM_GPU_ENODEV.
