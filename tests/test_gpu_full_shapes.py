@@ -1,7 +1,7 @@
 """Every payload of the BASELINE GPU shapes at full size, bit for bit against
 the oracle: the headline 65536 x 64 KiB (4 GiB), C3 8192 x 1 MiB CRC-64
 (8 GiB), C4 262144 x U[64 B, 64 KiB] offsets (8.6 GB) and C5 2^20 x 64 KiB
-(64 GiB, the whole 8-GPU batch on one GPU).
+(64 GiB, the whole 8-GPU batch on one GPU); plus single payloads past 2 GiB.
 
 The fixed shapes never leave the device: the oracle regenerates the same
 splitmix64 payload bytes on the host (oracle_splitmix_batch_fixed, 16
@@ -74,3 +74,24 @@ def test_c5_on_one_gpu_every_payload_and_split_calls(gpu, oracle_mod):
     del t
     assert np.array_equal(np.concatenate([lo, hi]).astype(np.uint64), got)
     assert _mismatches(got, _want_fixed(oracle_mod, "crc32c", SEED_C5, count, length)) == (0, [])
+
+
+@pytest.mark.parametrize("method", ["crc32c", "crc64"])
+def test_payloads_past_2_gib(gpu, oracle_mod, method):
+    """Single payloads of more than 2^31 bytes: a fixed batch of one (generic
+    and aligned window) and an offsets batch whose middle payload is > 2 GiB
+    (the offsets kernel's 64-bit-length path), next to small neighbours."""
+    import torch
+    big = (1 << 31) + 4096 * 3 + 5
+    t = torch.empty(big + (1 << 20) + 64, dtype=torch.uint8, device="cuda")
+    gpu.fill_splitmix(t, 0xB16)
+    host = t[:big + (1 << 20)].cpu().numpy()
+    variant = "sse42" if method == "crc32c" else "table"
+    for n in (big, (1 << 31) + (1 << 20)):  # ragged length / whole 4 KiB-ring steps
+        got = int(gpu.as_unsigned(gpu.checksum_fixed(method, t, n, count=1))[0])
+        assert got == oracle_mod.crc(method, host[:n], variant=variant), n
+    off = np.array([0, 100, 100 + big, 100 + big + 4097, 100 + big + 4097 + 3], dtype=np.uint64)
+    got = gpu.as_unsigned(gpu.checksum_offsets(method, t, torch.from_numpy(off.astype(np.int64)).cuda(),
+                                               offsets_host=off)).tolist()
+    want = [oracle_mod.crc(method, host[int(off[i]):int(off[i + 1])], variant=variant) for i in range(4)]
+    assert got == want
