@@ -245,6 +245,8 @@ __device__ unsigned long long g_mck_qdiag[4 * 64];
 __device__ unsigned int g_mck_qdiag_n;
 // per wave: fetches, fetch ticks (sum), fetch ticks (max), entry-wait ticks
 __device__ unsigned long long g_mck_qwave[6 * 16384];
+// per unit (u < 2^17): completion time | (blockIdx % 8) << 60 (tools/unit_timeline.py)
+__device__ unsigned long long g_mck_unit_end[1u << 17];
 #endif
 __device__ __noinline__ void queue_fault(uint32_t kind, uint64_t a, uint64_t b) {
     atomicAdd(&g_mck_queue_faults, 1u);
@@ -390,6 +392,7 @@ __device__ __forceinline__ void for_each_unit(WgQueue *L, unsigned long long *qu
 #if MCK_TRACE
             qs_busy += wall_clock64() - b0;
             qs_units += u < n;
+            if (l0 && u < n && u < (1ull << 17)) g_mck_unit_end[u] = wall_clock64() | (unsigned long long)(blockIdx.x % kQSub) << 60;
 #endif
         }
 #if MCK_TRACE

@@ -449,6 +449,11 @@ MCHECKSUM_PUBLIC int mck_debug_qwave_read(void *host, size_t bytes) {
     if (bytes > sizeof(g_mck_qwave)) bytes = sizeof(g_mck_qwave);
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_mck_qwave), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
+// ... the per-unit completion stamps of the last launch ...
+MCHECKSUM_PUBLIC int mck_debug_units_read(void *host, size_t bytes) {
+    if (bytes > sizeof(g_mck_unit_end)) bytes = sizeof(g_mck_unit_end);
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_mck_unit_end), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
 // ... and the work-queue fault records (count, then 4 words per record).
 MCHECKSUM_PUBLIC int mck_debug_qdiag_read(unsigned int *n, unsigned long long *rec) {
     if (hipMemcpyFromSymbol(n, HIP_SYMBOL(g_mck_qdiag_n), sizeof(*n), 0, hipMemcpyDeviceToHost) != hipSuccess) return -1;
