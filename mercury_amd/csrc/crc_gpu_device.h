@@ -758,9 +758,15 @@ __global__ __launch_bounds__(kBlk32<LIGHT>, 1) void crc32c_batch_kernel(BatchArg
     const uint64_t units = MODE == kOffsets ? a.count : (a.count + PPW - 1) / PPW;
     __shared__ WgQueue wgq;
     constexpr bool DYN = dyn_policy(32, MODE, NT, LIGHT);
+#if defined(MCK_EMPTY) && MCK_EMPTY == 2
+    if (!DYN) return;  // diagnostic: launch cost alone
+#endif
     if (DYN && threadIdx.x == 0) wg_queue_init(&wgq, a.queue, units);
     fill_lds32<LIGHT, kBlk32<LIGHT>>(lds_raw, pk);
     __syncthreads();
+#if defined(MCK_EMPTY) && MCK_EMPTY == 1
+    if (!DYN) return;  // diagnostic: launch + LDS table fill
+#endif
     MCK_STAMP(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6), 1);
     const Tab32<LIGHT> lds{lds_raw};
 
