@@ -1,0 +1,72 @@
+"""Batch entry points called from several host threads at once, the way
+Mercury's RPC handler threads would (Testing/unit/hg/mercury_unit.c:347-356:
+a handler thread pool).  A fresh process starts 8 threads that make their
+first library calls together, so the lazy per-device setup (table packs,
+work-queue ring; guarded by one mutex) and the work-queue slot allocation run
+concurrently.  Each thread uses its own stream and checks every result
+against the oracle."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+SCRIPT = r"""
+import sys, threading
+import numpy as np
+import torch
+sys.path.insert(0, sys.argv[1])
+from mercury_amd import gpu as G
+from oracle import oracle as O
+host = O.splitmix_bytes(32 << 20, 31337)
+dev = torch.cat([torch.from_numpy(host).cuda(), torch.zeros(64, dtype=torch.uint8, device="cuda")])
+rng = np.random.default_rng(5)
+jobs = []
+for k in range(8):
+    method = ("crc32c", "crc64")[k % 2]
+    offs = np.zeros(2001, dtype=np.uint64)
+    offs[1:] = np.cumsum(rng.integers(0, 8192, 2000))
+    jobs.append((method, offs, torch.from_numpy(offs.astype(np.int64)).cuda(),
+                 O.batch_offsets(method, host, offs, nthreads=4),
+                 O.batch_fixed(method, host, 4096, 4096, 4096, nthreads=4)))
+torch.cuda.synchronize()
+barrier = threading.Barrier(8)
+errors = []
+
+def worker(k):
+    method, offs, offs_d, want_o, want_f = jobs[k]
+    s = torch.cuda.Stream()
+    try:
+        barrier.wait()
+        for it in range(20):
+            with torch.cuda.stream(s):
+                o = G.checksum_offsets(method, dev, offs_d, stream=s)
+                f = G.checksum_fixed(method, dev, 4096, count=4096, stream=s)
+            s.synchronize()
+            if not np.array_equal(G.as_unsigned(o).astype(np.uint64), want_o):
+                errors.append((k, it, "offsets"))
+            if not np.array_equal(G.as_unsigned(f).astype(np.uint64), want_f):
+                errors.append((k, it, "fixed"))
+    except Exception as e:  # reported below
+        errors.append((k, repr(e)))
+
+th = [threading.Thread(target=worker, args=(k,)) for k in range(8)]
+for t in th:
+    t.start()
+for t in th:
+    t.join(timeout=90)
+assert not any(t.is_alive() for t in th), "a worker thread did not finish"
+assert not errors, errors[:5]
+assert G.queue_faults() == 0
+print("threads ok")
+"""
+
+
+def test_eight_host_threads_first_calls_together(gpu):
+    r = subprocess.run([sys.executable, "-c", SCRIPT, ROOT], capture_output=True, text=True, timeout=110,
+                       env=dict(os.environ, MCHECKSUM_GPU_LIGHT="0"))
+    assert r.returncode == 0 and "threads ok" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
