@@ -68,7 +68,7 @@ clean:
 
 # A/B variants of the batch kernels (tools/ab_variants.py).  Each is a full
 # libmchecksum built with different tuning macros.
-VARIANTS := base:-DMCK_RING=4 sdwa0:-DMCK_SDWA64=0 split1:-DMCK_CRC64_SPLIT=1 ring6:-DMCK_RING=6
+VARIANTS ?= base:-DMCK_RING=4 nib:-DMCK_CRC64_P6=0
 variants: $(COBJS) $(BUILD)/mchecksum_gpu_ext.o | $(BUILD)
 	mkdir -p $(BUILD)/variants
 	@for v in $(VARIANTS); do n=$${v%%:*}; f=$$(echo $${v#*:} | tr , " "); \
@@ -79,7 +79,8 @@ variants: $(COBJS) $(BUILD)/mchecksum_gpu_ext.o | $(BUILD)
 .PHONY: variants
 
 # The committed kernel sources at $(PREV) (all of csrc/ and include/) as
-# variant "prev" (A/B against the last commit).
+# variant "prev" (A/B against the last commit).  Its C objects are rebuilt
+# from the same sources: the table packs are shared structs.
 PREV ?= HEAD
 prev: $(COBJS) | $(BUILD)
 	rm -rf $(BUILD)/variants/prev_src && mkdir -p $(BUILD)/variants/prev_src
@@ -88,7 +89,11 @@ prev: $(COBJS) | $(BUILD)
 	  -c $(BUILD)/variants/prev_src/$(CSRC)/mchecksum_gpu.hip -o $(BUILD)/variants/gpu_prev.o
 	$(HIPCC) $(HIPFLAGS) -I$(BUILD)/variants/prev_src/include -I$(BUILD)/variants/prev_src/$(CSRC) \
 	  -c $(BUILD)/variants/prev_src/$(CSRC)/mchecksum_gpu_ext.hip -o $(BUILD)/variants/gpu_ext_prev.o
-	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $(BUILD)/variants/libmchecksum_prev.so $(COBJS) \
+	for f in $(notdir $(COBJS:.o=)); do $(CC) $(CFLAGS) -I$(BUILD)/variants/prev_src/include \
+	  -I$(BUILD)/variants/prev_src/$(CSRC) -c $(BUILD)/variants/prev_src/$(CSRC)/$$f.c \
+	  -o $(BUILD)/variants/prev_$$f.o || exit 1; done
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $(BUILD)/variants/libmchecksum_prev.so \
+	  $(addprefix $(BUILD)/variants/prev_,$(notdir $(COBJS))) \
 	  $(BUILD)/variants/gpu_prev.o $(BUILD)/variants/gpu_ext_prev.o -lpthread
 	cp $(LIB) $(BUILD)/variants/libmchecksum_cur.so
 .PHONY: variants prev

@@ -61,8 +61,26 @@ struct Tab32 {
 // pairs of ds_read_b64 (lanes that share an entry broadcast) -- conflict-free
 // without copies.  Tables p and p+4 share a 256-B block (p+4 at +8 B).  Then
 // the combine operators (nibble tables, 2 KiB each).
+//
+// MCK_CRC64_P6=1 instead looks a 64-bit word up in 12 tables (pack f5/f6):
+// bits 3..7 of each byte index a 32-entry table at 8-B stride -- one 256-B
+// row, entry v on bank pair v, conflict-free without copies, address =
+// (byte & 0xF8) --, and bits 0..2 of bytes 2i and 2i+1, gathered into one
+// 6-bit index by a shift + bit-select per 32-bit half, a 64-entry table
+// replicated 32x (entry v at v*256 B + lane copy, 16 KiB per table).  Three
+// quarters of the LDS reads of the nibble form; the combine operators then
+// move to global memory so two workgroups per CU still fit.
+#ifndef MCK_CRC64_P6
+#define MCK_CRC64_P6 1
+#endif
+#if MCK_CRC64_P6
+constexpr uint32_t kL64P5 = 0;
+constexpr uint32_t kL64P6 = 8 * 256;
+constexpr uint32_t kL64Main = kL64P6 + 4 * 16384;
+#else
 constexpr uint32_t kL64Hi = 32768;
 constexpr uint32_t kL64Main = kL64Hi + 4 * 256;
+#endif
 constexpr uint32_t kL64Bytes = kL64Main + CRC64_NOPS_MAX * 2048;
 // CRC-64 is VALU-bound (the table XOR tree); two 1024-thread workgroups per CU
 // (8 waves/SIMD, 80 KiB LDS each) hide the LDS latency.  MCK_CRC64_SPLIT=1
@@ -87,12 +105,17 @@ constexpr uint32_t kL64Bytes = kL64Main + CRC64_NOPS_MAX * 2048;
 #ifndef MCK_CRC64_OFF_TWO
 #define MCK_CRC64_OFF_TWO 1
 #endif
-constexpr int kRingOff64 = MCK_CRC64_OFF_TWO ? 4 : kRingOff;
+// Under MCK_CRC64_P6 the offsets path keeps its combine operators in LDS
+// (a dependent chain of 8 operator applications per payload: from global
+// memory C4-layout CRC-64 ran 21% slower), which leaves room for one
+// workgroup per CU.
+constexpr bool kCrc64OffTwo = MCK_CRC64_OFF_TWO && !MCK_CRC64_P6;
+constexpr int kRingOff64 = kCrc64OffTwo ? 4 : kRingOff;
 
 template <int W, int MODE, bool LIGHT = false>
 struct Shape {
-    static constexpr bool ops_global = W == 64 && MODE == 0 && MCK_CRC64_SPLIT;  // 0 = kFixedAligned
-    static constexpr bool two = W == 64 && (MODE == 0 || (MODE == 2 && MCK_CRC64_OFF_TWO));
+    static constexpr bool ops_global = W == 64 && MODE == 0 && (MCK_CRC64_SPLIT || MCK_CRC64_P6);  // 0 = kFixedAligned
+    static constexpr bool two = W == 64 && (MODE == 0 || (MODE == 2 && kCrc64OffTwo));
     static constexpr int block = LIGHT ? kLightBlock : two ? MCK_BLOCK64 : kBlock;
     static constexpr int blocks_per_cu = LIGHT ? 8 : two ? 2 : 1;
     static constexpr uint32_t lds64_bytes = ops_global ? kL64Main : kL64Bytes;
@@ -882,6 +905,7 @@ __device__ __forceinline__ void sdwa_lo(uint32_t &a, uint32_t x) {
     else sdwa_lo3(a, x);
 }
 
+#if !MCK_CRC64_P6
 template <int B>
 __device__ __forceinline__ void f64x_byte(const uint8_t *lds, uint32_t xl, uint32_t xh, Lane64 &ln, uint64_t *r) {
 #if MCK_SDWA64
@@ -902,7 +926,57 @@ __device__ __forceinline__ void f64x_byte(const uint8_t *lds, uint32_t xl, uint3
     r[4 * B + 3] = lds64(lds, __builtin_amdgcn_perm(h1, h1, sh) + kL64Hi + B * 256 + 8);
 #endif
 }
+#endif
 
+#if MCK_CRC64_P6
+// (byte B of x) & 0xF8: a 5-bit field scaled by 8, its own f5 address;
+// (byte B of t) & 0x3F into byte 1 of the lane-copy register a.
+#define MCK_SDWA_P6(B)                                                                              \
+    __device__ __forceinline__ uint32_t sdwa_f8_##B(uint32_t x) {                                   \
+        uint32_t r;                                                                                 \
+        asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD "         \
+            "src1_sel:BYTE_" #B : "=v"(r) : "s"(0xF8u), "v"(x));                                    \
+        return r;                                                                                   \
+    }                                                                                               \
+    __device__ __forceinline__ void sdwa_p6_##B(uint32_t &a, uint32_t t) {                          \
+        asm("v_and_b32_sdwa %0, %1, %2 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD "   \
+            "src1_sel:BYTE_" #B : "+v"(a) : "s"(0x3Fu), "v"(t));                                    \
+    }
+MCK_SDWA_P6(0)
+MCK_SDWA_P6(1)
+MCK_SDWA_P6(2)
+MCK_SDWA_P6(3)
+#undef MCK_SDWA_P6
+__device__ __forceinline__ uint64_t xor13(const uint64_t *r, uint64_t extra) {
+    const uint64_t a = xor3_64(r[0], r[1], r[2]), b = xor3_64(r[3], r[4], r[5]), c = xor3_64(r[6], r[7], r[8]);
+    return xor3_64(a, b, xor3_64(c, xor3_64(r[9], r[10], r[11]), extra));
+}
+// Z^(16G)(x) ^ next from the 12 tables f5/f6 (LDS map above).
+__device__ __forceinline__ uint64_t f64x(const uint8_t *lds, uint64_t x, uint64_t next, Lane64 &ln) {
+    const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
+    // byte 2i' of t: bits 0..2 of bytes 2i', 2i'+1 of the half (bit-select)
+    const uint32_t tl = (xl & 0x07070707u) | ((xl >> 5) & ~0x07070707u);
+    const uint32_t th = (xh & 0x07070707u) | ((xh >> 5) & ~0x07070707u);
+    uint64_t r[12];
+    r[0] = lds64(lds, sdwa_f8_0(xl) + kL64P5 + 0 * 256);
+    r[1] = lds64(lds, sdwa_f8_1(xl) + kL64P5 + 1 * 256);
+    r[2] = lds64(lds, sdwa_f8_2(xl) + kL64P5 + 2 * 256);
+    r[3] = lds64(lds, sdwa_f8_3(xl) + kL64P5 + 3 * 256);
+    r[4] = lds64(lds, sdwa_f8_0(xh) + kL64P5 + 4 * 256);
+    r[5] = lds64(lds, sdwa_f8_1(xh) + kL64P5 + 5 * 256);
+    r[6] = lds64(lds, sdwa_f8_2(xh) + kL64P5 + 6 * 256);
+    r[7] = lds64(lds, sdwa_f8_3(xh) + kL64P5 + 7 * 256);
+    sdwa_p6_0(ln.al[0], tl);
+    r[8] = lds64(lds, ln.al[0] + kL64P6 + 0 * 16384);
+    sdwa_p6_2(ln.al[1], tl);
+    r[9] = lds64(lds, ln.al[1] + kL64P6 + 1 * 16384);
+    sdwa_p6_0(ln.al[2], th);
+    r[10] = lds64(lds, ln.al[2] + kL64P6 + 2 * 16384);
+    sdwa_p6_2(ln.al[3], th);
+    r[11] = lds64(lds, ln.al[3] + kL64P6 + 3 * 16384);
+    return xor13(r, next);
+}
+#else
 // Z^(16G)(x) ^ next from the 16 nibble tables (LDS map above): one VALU op per
 // lookup to form its address, 8 v_bitop3 per 32-bit half for the XOR tree.
 __device__ __forceinline__ uint64_t f64x(const uint8_t *lds, uint64_t x, uint64_t next, Lane64 &ln) {
@@ -914,6 +988,10 @@ __device__ __forceinline__ uint64_t f64x(const uint8_t *lds, uint64_t x, uint64_
     f64x_byte<3>(lds, xl, xh, ln, r);
     return xor17(r, next);
 }
+#endif
+
+// generic / offsets paths: operators from LDS
+constexpr bool kOps64Global = false;
 
 template <bool OG>
 __device__ __forceinline__ uint64_t op64(const uint8_t *lds, const crc64_gpu_pack_t *pk, uint32_t o, uint64_t x) {
@@ -948,6 +1026,14 @@ template <int BLOCK, bool OG>
 __device__ void fill_lds64(uint8_t *lds, const crc64_gpu_pack_t *pk) {
     uint64_t *l = reinterpret_cast<uint64_t *>(lds);
     uint4 *l4 = reinterpret_cast<uint4 *>(lds);
+#if MCK_CRC64_P6
+    // f6: entry v of table i at i*16 KiB + v*256 B, 32 copies (two per 16-B write)
+    for (uint32_t q = threadIdx.x; q < 4096u; q += BLOCK) {
+        const uint64_t v = pk->f6[q >> 10][(q >> 4) & 63u];
+        l4[kL64P6 / 16 + q] = make_uint4((uint32_t)v, (uint32_t)(v >> 32), (uint32_t)v, (uint32_t)(v >> 32));
+    }
+    for (uint32_t d = threadIdx.x; d < 256u; d += BLOCK) l[kL64P5 / 8 + d] = pk->f5[d >> 5][d & 31u];
+#else
     // low-nibble tables (main[2p]), 32 copies (two per ds_write_b128);
     // high-nibble tables (main[2p+1]) at 16-B entry stride
     for (uint32_t q = threadIdx.x; q < 2048u; q += BLOCK) {
@@ -959,6 +1045,7 @@ __device__ void fill_lds64(uint8_t *lds, const crc64_gpu_pack_t *pk) {
         const uint32_t p = d >> 4, v = d & 15u;  // table p, entry v
         l[kL64Hi / 8 + (p & 3u) * 32 + (p >> 2) + v * 2] = pk->main[2 * p + 1][v];
     }
+#endif
     if constexpr (!OG) {
         const uint4 *ops = reinterpret_cast<const uint4 *>(&pk->ops[0][0][0]);
         const uint32_t nops = pk->nops * 128u;
@@ -1074,8 +1161,8 @@ __device__ __forceinline__ uint64_t payload64_generic(const uint8_t *lds, const 
             }
         }
     }
-    uint64_t x = combine64<LOG2G, false>(lds, pk, x0, x1, gl);
-    x = op64<false>(lds, pk, 1 + LOG2G + (uint32_t)(a1 - ea), x);
+    uint64_t x = combine64<LOG2G, kOps64Global>(lds, pk, x0, x1, gl);
+    x = op64<kOps64Global>(lds, pk, 1 + LOG2G + (uint32_t)(a1 - ea), x);
     if (len < 8) x ^= pk->zinit[len];
     return x;
 }
@@ -1128,8 +1215,8 @@ __device__ __forceinline__ uint64_t payload64_g64(const uint8_t *lds, const crc6
             }
         }
     }
-    uint64_t x = combine64<6, false>(lds, pk, x0, x1, gl);
-    x = op64<false>(lds, pk, 1 + 6 + (uint32_t)(a1 - ea), x);
+    uint64_t x = combine64<6, kOps64Global>(lds, pk, x0, x1, gl);
+    x = op64<kOps64Global>(lds, pk, 1 + 6 + (uint32_t)(a1 - ea), x);
     if (!RAW && len < 8) x ^= pk->zinit[len];
     return x;
 }

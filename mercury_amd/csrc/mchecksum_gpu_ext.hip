@@ -335,10 +335,13 @@ __global__ __launch_bounds__(1024, kSegWavesPerEU<W * 4 + PART>) void seg_kernel
         }
         seg_object_terms<32>(a);
     } else {
-        __shared__ __attribute__((aligned(16))) uint8_t lds[kL64Bytes];
+        // aligned chunks under the 12-lookup fold: combine operators from
+        // global memory (once per 256 KiB chunk), so two workgroups fit a CU
+        constexpr bool OG = PART == 1 && MCK_CRC64_P6;
+        __shared__ __attribute__((aligned(16))) uint8_t lds[OG ? kL64Main : kL64Bytes];
         const crc64_gpu_pack_t *pk = reinterpret_cast<const crc64_gpu_pack_t *>(a.pack);
         const crc64_shift_pack_t *sp = reinterpret_cast<const crc64_shift_pack_t *>(a.shift);
-        fill_lds64<1024, false>(lds, pk);
+        fill_lds64<1024, OG>(lds, pk);
         __syncthreads();
         const uint32_t lc = (lane & 31u) << 3;
         unsigned long long *out = reinterpret_cast<unsigned long long *>(a.out);
@@ -358,8 +361,8 @@ __global__ __launch_bounds__(1024, kSegWavesPerEU<W * 4 + PART>) void seg_kernel
             if (aligned != (PART == 1)) continue;
             uint64_t x;
             if constexpr (PART == 1)
-                x = nt ? payload64_aligned<6, true, false>(lds, pk, q, (uint32_t)(n >> 10), lane, lc, 0ull)
-                       : payload64_aligned<6, false, false>(lds, pk, q, (uint32_t)(n >> 10), lane, lc, 0ull);
+                x = nt ? payload64_aligned<6, true, OG>(lds, pk, q, (uint32_t)(n >> 10), lane, lc, 0ull)
+                       : payload64_aligned<6, false, OG>(lds, pk, q, (uint32_t)(n >> 10), lane, lc, 0ull);
             else
                 x = payload64_g64<false, true>(lds, pk, q, n, lane, lc);
             x = shift64(sp, uniform(x), after);

@@ -96,10 +96,18 @@ extern "C" uint64_t emu_crc64(const crc64_gpu_pack_t *pk, const uint8_t *buf, in
             if (!mck_piece_clean(pc, hs, he, 8))
                 for (int j = 0; j < 2; j++) w[j] = mck_mask64(w[j], pc - hs + 8 * j, len, pk->init);
             for (int j = 0; j < 2; j++) {
-                uint64_t x = S[2 * l + j] ^ w[j], r = 0;
+                uint64_t x = S[2 * l + j] ^ w[j], r = 0, r6 = 0;
                 for (int p = 0; p < 8; p++)
                     for (int h = 0; h < 2; h++) r ^= pk->main[2 * p + h][(x >> (8 * p + 4 * h)) & 15];
-                S[2 * l + j] = r;
+                // the kernels' 12-lookup form (f5 / f6) of the same fold
+                for (int p = 0; p < 8; p++) r6 ^= pk->f5[p][(x >> (8 * p + 3)) & 31];
+                for (int i = 0; i < 4; i++)
+                    r6 ^= pk->f6[i][((x >> (16 * i)) & 7) | (((x >> (16 * i + 8)) & 7) << 3)];
+                if (r6 != r) {
+                    std::fprintf(stderr, "emu_crc64: f5/f6 fold differs from the nibble fold\n");
+                    std::abort();
+                }
+                S[2 * l + j] = r6;
             }
         }
     std::vector<uint64_t> X(G);
