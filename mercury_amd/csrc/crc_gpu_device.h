@@ -82,10 +82,10 @@ constexpr uint32_t kL64Hi = 32768;
 constexpr uint32_t kL64Main = kL64Hi + 4 * 256;
 #endif
 constexpr uint32_t kL64Bytes = kL64Main + CRC64_NOPS_MAX * 2048;
-// CRC-64 is VALU-bound (the table XOR tree); two 1024-thread workgroups per CU
-// (8 waves/SIMD, 80 KiB LDS each) hide the LDS latency.  MCK_CRC64_SPLIT=1
-// reads the combine operators (touched once per payload) from global memory
-// instead of LDS on the aligned path.
+// CRC-64 is LDS/VALU-bound (table reads and their XOR tree); two 1024-thread
+// workgroups per CU (8 waves/SIMD) hide the LDS latency.  MCK_CRC64_SPLIT=1
+// (implied by MCK_CRC64_P6) reads the combine operators (touched once per
+// payload) from global memory instead of LDS on the aligned path.
 #ifndef MCK_CRC64_SPLIT
 #define MCK_CRC64_SPLIT 0
 #endif
