@@ -105,12 +105,23 @@ constexpr uint32_t kL64Bytes = kL64Main + CRC64_NOPS_MAX * 2048;
 #ifndef MCK_CRC64_OFF_TWO
 #define MCK_CRC64_OFF_TWO 1
 #endif
-// Under MCK_CRC64_P6 the offsets path keeps its combine operators in LDS
-// (a dependent chain of 8 operator applications per payload: from global
-// memory C4-layout CRC-64 ran 21% slower), which leaves room for one
-// workgroup per CU.
-constexpr bool kCrc64OffTwo = MCK_CRC64_OFF_TWO && !MCK_CRC64_P6;
+// Under MCK_CRC64_P6 the offsets path cannot read all its combine operators
+// from global memory (a dependent chain of 8 operator applications per
+// payload: C4-layout CRC-64 ran 21% slower) and all of them in LDS leave room
+// for only one workgroup per CU.
+// MCK_CRC64_OFF_MIX=1 instead keeps only the six butterfly operators in LDS
+// (12 KiB: 79.9 KiB in all) and reads Z^-8 and the tail operator, the two
+// ends of the chain, from global memory: two workgroups per CU again, +6% on
+// C4-layout CRC-64 (profiles/r01/ab20_crc64_offsets_mix.log).
+#ifndef MCK_CRC64_OFF_MIX
+#define MCK_CRC64_OFF_MIX 1
+#endif
+constexpr bool kCrc64OffMix = MCK_CRC64_P6 && MCK_CRC64_OFF_MIX;
+constexpr bool kCrc64OffTwo = (MCK_CRC64_OFF_TWO && !MCK_CRC64_P6) || kCrc64OffMix;
 constexpr int kRingOff64 = kCrc64OffTwo ? 4 : kRingOff;
+// where the CRC-64 combine operators live: all in LDS, all in global memory,
+// or the butterflies (ops 1..6) in LDS and the rest global
+enum OpsMode : int { kOpsLds = 0, kOpsGlobal = 1, kOpsMix = 2 };
 
 template <int W, int MODE, bool LIGHT = false>
 struct Shape {
@@ -118,7 +129,10 @@ struct Shape {
     static constexpr bool two = W == 64 && (MODE == 0 || (MODE == 2 && kCrc64OffTwo));
     static constexpr int block = LIGHT ? kLightBlock : two ? MCK_BLOCK64 : kBlock;
     static constexpr int blocks_per_cu = LIGHT ? 8 : two ? 2 : 1;
-    static constexpr uint32_t lds64_bytes = ops_global ? kL64Main : kL64Bytes;
+    static constexpr int ops_mode = ops_global ? kOpsGlobal : (W == 64 && MODE == 2 && kCrc64OffMix) ? kOpsMix : kOpsLds;
+    static constexpr uint32_t lds64_bytes = ops_mode == kOpsGlobal ? kL64Main
+                                          : ops_mode == kOpsMix    ? kL64Main + 6 * 2048
+                                                                   : kL64Bytes;
 };
 // single-argument aliases (a comma inside __launch_bounds__ splits the macro)
 template <int MODE>
@@ -990,9 +1004,6 @@ __device__ __forceinline__ uint64_t f64x(const uint8_t *lds, uint64_t x, uint64_
 }
 #endif
 
-// generic / offsets paths: operators from LDS
-constexpr bool kOps64Global = false;
-
 template <bool OG>
 __device__ __forceinline__ uint64_t op64(const uint8_t *lds, const crc64_gpu_pack_t *pk, uint32_t o, uint64_t x) {
     uint64_t r[16];
@@ -1008,21 +1019,31 @@ __device__ __forceinline__ uint64_t op64(const uint8_t *lds, const crc64_gpu_pac
     return xor17(r, 0);
 }
 
-template <int LOG2G, bool OG>
+template <int OM>
+__device__ __forceinline__ uint64_t opm64(const uint8_t *lds, const crc64_gpu_pack_t *pk, uint32_t o, uint64_t x) {
+    if constexpr (OM == kOpsMix) {
+        if (o >= 1 && o <= 6) return op64<false>(lds, pk, o - 1, x);  // butterflies at kL64Main
+        return op64<true>(lds, pk, o, x);
+    } else {
+        return op64<OM == kOpsGlobal>(lds, pk, o, x);
+    }
+}
+
+template <int LOG2G, int OM>
 __device__ __forceinline__ uint64_t combine64(const uint8_t *lds, const crc64_gpu_pack_t *pk, uint64_t s0, uint64_t s1,
                                               uint32_t gl) {
-    uint64_t x = s0 ^ op64<OG>(lds, pk, 0, s1);
+    uint64_t x = s0 ^ opm64<OM>(lds, pk, 0, s1);
 #pragma unroll
     for (int k = 0; k < LOG2G; k++) {
         const uint64_t other = __shfl_xor(x, 1 << k, 64);
         const bool bit = (gl >> k) & 1u;
         const uint64_t lo = bit ? other : x, hi = bit ? x : other;
-        x = lo ^ op64<OG>(lds, pk, 1 + k, hi);
+        x = lo ^ opm64<OM>(lds, pk, 1 + k, hi);
     }
     return x;
 }
 
-template <int BLOCK, bool OG>
+template <int BLOCK, int OM>
 __device__ void fill_lds64(uint8_t *lds, const crc64_gpu_pack_t *pk) {
     uint64_t *l = reinterpret_cast<uint64_t *>(lds);
     uint4 *l4 = reinterpret_cast<uint4 *>(lds);
@@ -1046,10 +1067,13 @@ __device__ void fill_lds64(uint8_t *lds, const crc64_gpu_pack_t *pk) {
         l[kL64Hi / 8 + (p & 3u) * 32 + (p >> 2) + v * 2] = pk->main[2 * p + 1][v];
     }
 #endif
-    if constexpr (!OG) {
+    if constexpr (OM == kOpsLds) {
         const uint4 *ops = reinterpret_cast<const uint4 *>(&pk->ops[0][0][0]);
         const uint32_t nops = pk->nops * 128u;
         for (uint32_t q = threadIdx.x; q < nops; q += BLOCK) l4[kL64Main / 16 + q] = ops[q];
+    } else if constexpr (OM == kOpsMix) {  // ops 1..6 (needs G = 64: nops >= 7)
+        const uint4 *ops = reinterpret_cast<const uint4 *>(&pk->ops[1][0][0]);
+        for (uint32_t q = threadIdx.x; q < 6u * 128u; q += BLOCK) l4[kL64Main / 16 + q] = ops[q];
     }
 }
 
@@ -1108,7 +1132,7 @@ __device__ __forceinline__ uint64_t payload64_aligned(const uint8_t *lds, const 
     return combine64<LOG2G, OG>(lds, pk, x0, x1, gl);
 }
 
-template <int LOG2G, bool NT>
+template <int LOG2G, bool NT, int OM = kOpsLds>
 __device__ __forceinline__ uint64_t payload64_generic(const uint8_t *lds, const crc64_gpu_pack_t *pk,
                                                       const uint8_t *p, uint64_t len, uint32_t gl, uint32_t lc) {
     constexpr int G = 1 << LOG2G;
@@ -1161,14 +1185,14 @@ __device__ __forceinline__ uint64_t payload64_generic(const uint8_t *lds, const 
             }
         }
     }
-    uint64_t x = combine64<LOG2G, kOps64Global>(lds, pk, x0, x1, gl);
-    x = op64<kOps64Global>(lds, pk, 1 + LOG2G + (uint32_t)(a1 - ea), x);
+    uint64_t x = combine64<LOG2G, OM>(lds, pk, x0, x1, gl);
+    x = opm64<OM>(lds, pk, 1 + LOG2G + (uint32_t)(a1 - ea), x);
     if (len < 8) x ^= pk->zinit[len];
     return x;
 }
 
 // CRC-64 counterpart of payload32_g64.
-template <bool NT, bool RAW = false>
+template <bool NT, bool RAW = false, int OM = kOpsLds>
 __device__ __forceinline__ uint64_t payload64_g64(const uint8_t *lds, const crc64_gpu_pack_t *pk, const uint8_t *p,
                                                   uint64_t len, uint32_t gl, uint32_t lc) {
     const uint64_t init = RAW ? 0ull : pk->init;
@@ -1215,8 +1239,8 @@ __device__ __forceinline__ uint64_t payload64_g64(const uint8_t *lds, const crc6
             }
         }
     }
-    uint64_t x = combine64<6, kOps64Global>(lds, pk, x0, x1, gl);
-    x = op64<kOps64Global>(lds, pk, 1 + 6 + (uint32_t)(a1 - ea), x);
+    uint64_t x = combine64<6, OM>(lds, pk, x0, x1, gl);
+    x = opm64<OM>(lds, pk, 1 + 6 + (uint32_t)(a1 - ea), x);
     if (!RAW && len < 8) x ^= pk->zinit[len];
     return x;
 }
@@ -1232,7 +1256,7 @@ __global__ __launch_bounds__(kBlk64<MODE>, kWpe64<MODE>) void crc64_batch_kernel
     __shared__ WgQueue wgq;
     constexpr bool DYN = dyn_policy(64, MODE, NT, false);
     if (DYN && threadIdx.x == 0) wg_queue_init(&wgq, a.queue, units);
-    fill_lds64<S::block, S::ops_global>(lds, pk);
+    fill_lds64<S::block, S::ops_mode>(lds, pk);
     __syncthreads();
 
     const uint32_t lane = threadIdx.x & 63u;
@@ -1246,8 +1270,8 @@ __global__ __launch_bounds__(kBlk64<MODE>, kWpe64<MODE>) void crc64_batch_kernel
         auto one = [&](uint64_t p) {
             const uint64_t o = a.offsets[p];
             const uint64_t n = a.offsets[p + 1] - o;
-            const uint64_t x = n < (1ull << 31) ? payload64_g64<NT>(lds, pk, a.base + o, n, gl, lc)
-                                                : payload64_generic<LOG2G, NT>(lds, pk, a.base + o, n, gl, lc);
+            const uint64_t x = n < (1ull << 31) ? payload64_g64<NT, false, S::ops_mode>(lds, pk, a.base + o, n, gl, lc)
+                                                : payload64_generic<LOG2G, NT, S::ops_mode>(lds, pk, a.base + o, n, gl, lc);
             if (gl == 0) emit<uint64_t, VERIFY>(a, p, x ^ xorout);
         };
         for_each_unit<true>(&wgq, a.queue, units, wave, nw, one);

@@ -341,7 +341,7 @@ __global__ __launch_bounds__(1024, kSegWavesPerEU<W * 4 + PART>) void seg_kernel
         __shared__ __attribute__((aligned(16))) uint8_t lds[OG ? kL64Main : kL64Bytes];
         const crc64_gpu_pack_t *pk = reinterpret_cast<const crc64_gpu_pack_t *>(a.pack);
         const crc64_shift_pack_t *sp = reinterpret_cast<const crc64_shift_pack_t *>(a.shift);
-        fill_lds64<1024, OG>(lds, pk);
+        fill_lds64<1024, OG ? kOpsGlobal : kOpsLds>(lds, pk);
         __syncthreads();
         const uint32_t lc = (lane & 31u) << 3;
         unsigned long long *out = reinterpret_cast<unsigned long long *>(a.out);
