@@ -1263,8 +1263,14 @@ __global__ __launch_bounds__(kBlk64<MODE>, kWpe64<MODE>) void crc64_batch_kernel
     const uint32_t gl = lane & ((1u << LOG2G) - 1u), grp = lane >> LOG2G;
     const uint32_t lc = (lane & 31u) << 3;
     const uint64_t xorout = pk->xorout;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWPB + (threadIdx.x >> 6));
     const uint32_t nw = gridDim.x * kWPB;
+    // A static split with fewer units than waves numbers the waves across
+    // workgroups first, so a small batch spreads over CUs (the host then
+    // launches one workgroup per unit) instead of filling one CU's LDS
+    // pipe: 64 x 4 KiB took 18.4 us packed into one workgroup.
+    const bool spread = !DYN && units < nw;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(spread ? (threadIdx.x >> 6) * gridDim.x + blockIdx.x
+                                                                : blockIdx.x * kWPB + (threadIdx.x >> 6));
 
     if (MODE == kOffsets) {
         auto one = [&](uint64_t p) {

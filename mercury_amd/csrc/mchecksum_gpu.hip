@@ -337,7 +337,15 @@ int launch_fixed(DevCtx *c, const void *pack, int width, int lg, const void *dev
     const uint64_t ppw = 64u >> lg;
     if (dyn_policy(width, aligned ? kFixedAligned : kFixedGeneric, nt, light) && !(a.queue = queue_slot(c, stream)))
         return MCHECKSUM_GPU_EINVAL;
-    return launch(k, a, grid_for(c, (count + ppw - 1) / ppw, k), stream);
+    const uint64_t units = (count + ppw - 1) / ppw;
+    unsigned blocks = grid_for(c, units, k);
+    // CRC-64 static split with fewer units than one full workgroup per CU:
+    // one workgroup per unit, at most one per CU (each pays a 66 KiB LDS
+    // fill); the kernel then numbers waves across workgroups first
+    if (width == 64 && !dyn_policy(width, aligned ? kFixedAligned : kFixedGeneric, nt, false) &&
+        units < (uint64_t)c->cus * (uint64_t)(k.block / 64))
+        blocks = (unsigned)(units < (uint64_t)c->cus ? (units ? units : 1) : c->cus);
+    return launch(k, a, blocks, stream);
 }
 
 }  // namespace mck
