@@ -256,9 +256,12 @@ struct WgQueue {
     unsigned long long entry[kWgRing];  // (chunk seq << 32) | global chunk id
 };
 
+// (readfirstlane returns int: widen each half as uint32_t, or a low half with
+// bit 31 set would sign-extend over the high half)
 __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
-    return (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32 |
-           __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
+    return (uint64_t)hi << 32 | lo;
 }
 
 template <class T>
@@ -522,6 +525,18 @@ __device__ __forceinline__ uint32_t f32s(Tab32<true> t, uint32_t x, uint32_t, ui
     return xor3(lds32(t.lds, a0), lds32(t.lds, a1 + 1024), lds32(t.lds, a2 + 2048)) ^ lds32(t.lds, a3 + 3072);
 }
 
+// Z^(16G)(x) ^ extra: the fourth lookup and the next data word share one bitop3.
+__device__ __forceinline__ uint32_t f32sx(Tab32<false> t, uint32_t x, uint32_t extra, uint32_t lc0, uint32_t lc1) {
+    const uint32_t a0 = __builtin_amdgcn_perm(x, lc0, 0x0C020400u);
+    const uint32_t a1 = __builtin_amdgcn_perm(x, lc0, 0x0C020500u);
+    const uint32_t a2 = __builtin_amdgcn_perm(x, lc1, 0x0C020600u);
+    const uint32_t a3 = __builtin_amdgcn_perm(x, lc1, 0x0C020700u);
+    return xor3(xor3(lds32(t.lds, a0), lds32(t.lds, a1 + 128), lds32(t.lds, a2)), lds32(t.lds, a3 + 128), extra);
+}
+__device__ __forceinline__ uint32_t f32sx(Tab32<true> t, uint32_t x, uint32_t extra, uint32_t lc0, uint32_t lc1) {
+    return f32s(t, x, lc0, lc1) ^ extra;
+}
+
 template <bool LIGHT>
 __device__ __forceinline__ uint32_t op32(Tab32<LIGHT> tab, uint32_t o, uint32_t x) {
     const uint32_t base = (LIGHT ? kL32LightMain : kL32Main) + o * 512;
@@ -574,6 +589,105 @@ __device__ void fill_lds32(uint8_t *lds, const crc32_gpu_pack_t *pk) {
 //
 // Aligned fixed-size payload: base 16-B aligned, len = K * 16G, no masking,
 // no pad bytes (tail op is the identity and is skipped).
+#ifndef MCK_ALIGNED32_V2
+#define MCK_ALIGNED32_V2 1
+#endif
+#ifndef MCK_LA32
+#define MCK_LA32 0
+#endif
+// Global-address-space views: loads through them are global_load (never
+// flat_load, which would also count against lgkmcnt and make every LDS wait
+// wait for HBM), and a wave-uniform base in SGPRs gives the saddr form.
+typedef const __attribute__((address_space(1))) uint8_t *gbyte_t;
+typedef const __attribute__((address_space(1))) u32x4_t *gvec_t;
+__device__ __forceinline__ gbyte_t global_ptr(const uint8_t *p, bool uniform) {
+    const uint64_t v = reinterpret_cast<uint64_t>(p);
+    return (gbyte_t)(uniform ? uniform64(v) : v);
+}
+template <bool NT>
+__device__ __forceinline__ uint4 ldg16(gbyte_t p) {
+    const gvec_t q = (gvec_t)p;
+    u32x4_t v;
+    if constexpr (NT) v = __builtin_nontemporal_load(q);
+    else v = *q;
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+#if MCK_ALIGNED32_V2
+// Aligned step loop without per-step tests: K is a multiple of kRing and
+// >= kRing (launch_fixed's aligned test), so every load of the steady loop is
+// in range and the last kRing steps run without loads.  The load pointer
+// advances by kRing steps per iteration (for G = 64 a wave-uniform SGPR pair:
+// saddr loads with the lane offset in one VGPR and the slot in the immediate).
+// Each slot's data word is folded into the state before the slot is reloaded,
+// so the ring needs no register copies.
+template <int LOG2G, bool NT, class TAB>
+__device__ __forceinline__ uint32_t payload32_aligned(TAB lds, const uint8_t *p, uint64_t K64, uint32_t gl,
+                                                      uint32_t lc0, uint32_t lc1, uint32_t init) {
+    constexpr uint32_t G = 1u << LOG2G;
+    constexpr uint32_t R = kRing;
+    constexpr uint32_t S = 16u * G;  // bytes per step
+    const uint32_t K = (uint32_t)K64;
+    gbyte_t lb = global_ptr(p, LOG2G == 6);
+    const uint32_t lo = 16u * gl;
+    uint4 ring[R];
+#pragma unroll
+    for (uint32_t u = 0; u < R; u++) ring[u] = ldg16<NT>(lb + (lo + u * S));
+    lb += R * S;
+    uint32_t x0 = gl == 0 ? init : 0u, x1 = 0, x2 = 0, x3 = 0;
+#if MCK_LA32
+    // look-ahead: y holds state ^ (data of the step about to run), and the
+    // next step's data word rides in the table-XOR tree (2 v_bitop3, no XOR)
+    uint32_t y0 = x0 ^ ring[0].x, y1 = ring[0].y, y2 = ring[0].z, y3 = ring[0].w;
+    for (uint32_t k = R; k < K; k += R) {
+#pragma unroll
+        for (uint32_t u = 0; u < R; u++) {
+            ring[u] = ldg16<NT>(lb + (lo + u * S));
+            const uint4 nx = ring[(u + 1) % R];
+            y0 = f32sx(lds, y0, nx.x, lc0, lc1);
+            y1 = f32sx(lds, y1, nx.y, lc0, lc1);
+            y2 = f32sx(lds, y2, nx.z, lc0, lc1);
+            y3 = f32sx(lds, y3, nx.w, lc0, lc1);
+        }
+        lb += R * S;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u + 1 < R; u++) {
+        const uint4 nx = ring[u + 1];
+        y0 = f32sx(lds, y0, nx.x, lc0, lc1);
+        y1 = f32sx(lds, y1, nx.y, lc0, lc1);
+        y2 = f32sx(lds, y2, nx.z, lc0, lc1);
+        y3 = f32sx(lds, y3, nx.w, lc0, lc1);
+    }
+    x0 = f32s(lds, y0, lc0, lc1);
+    x1 = f32s(lds, y1, lc0, lc1);
+    x2 = f32s(lds, y2, lc0, lc1);
+    x3 = f32s(lds, y3, lc0, lc1);
+    return combine32<LOG2G>(lds, x0, x1, x2, x3, gl);
+#else
+    for (uint32_t k = R; k < K; k += R) {
+#pragma unroll
+        for (uint32_t u = 0; u < R; u++) {
+            const uint32_t y0 = x0 ^ ring[u].x, y1 = x1 ^ ring[u].y, y2 = x2 ^ ring[u].z, y3 = x3 ^ ring[u].w;
+            ring[u] = ldg16<NT>(lb + (lo + u * S));
+            x0 = f32s(lds, y0, lc0, lc1);
+            x1 = f32s(lds, y1, lc0, lc1);
+            x2 = f32s(lds, y2, lc0, lc1);
+            x3 = f32s(lds, y3, lc0, lc1);
+        }
+        lb += R * S;
+    }
+#endif
+#pragma unroll
+    for (uint32_t u = 0; u < R; u++) {
+        x0 = f32s(lds, x0 ^ ring[u].x, lc0, lc1);
+        x1 = f32s(lds, x1 ^ ring[u].y, lc0, lc1);
+        x2 = f32s(lds, x2 ^ ring[u].z, lc0, lc1);
+        x3 = f32s(lds, x3 ^ ring[u].w, lc0, lc1);
+    }
+    return combine32<LOG2G>(lds, x0, x1, x2, x3, gl);
+}
+#else
 template <int LOG2G, bool NT, class TAB>
 __device__ __forceinline__ uint32_t payload32_aligned(TAB lds, const uint8_t *p, uint64_t K, uint32_t gl,
                                                       uint32_t lc0, uint32_t lc1, uint32_t init) {
@@ -599,6 +713,7 @@ __device__ __forceinline__ uint32_t payload32_aligned(TAB lds, const uint8_t *p,
     }
     return combine32<LOG2G>(lds, x0, x1, x2, x3, gl);
 }
+#endif
 
 template <typename T>
 __device__ __forceinline__ T wave_max(T v) {

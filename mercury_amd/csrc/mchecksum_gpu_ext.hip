@@ -324,9 +324,9 @@ __global__ __launch_bounds__(1024, kSegWavesPerEU<W * 4 + PART>) void seg_kernel
         while (walk.next(&p, &n, &in, &j, &after)) {
             if (!in) continue;
             const uint8_t *q = reinterpret_cast<const uint8_t *>(p);
-            // whole 1 KiB steps from a 16-B aligned start (the usual bulk
-            // segment) take the aligned loop: no edge masks, no pad operator
-            const bool aligned = p % 16 == 0 && n % 1024 == 0;
+            // whole rings of 1 KiB steps from a 16-B aligned start (the usual
+            // bulk segment) take the aligned loop: no edge masks, no pad operator
+            const bool aligned = p % 16 == 0 && n % (1024u * kRing) == 0 && n != 0;
             uint32_t x = aligned && nt    ? payload32_aligned<6, true>(lds, q, n >> 10, lane, lc0, lc1, 0u)
                          : aligned        ? payload32_aligned<6, false>(lds, q, n >> 10, lane, lc0, lc1, 0u)
                                           : payload32_g64<false, Tab32<false>, true>(lds, pk, q, n, lane, lc0, lc1);
