@@ -18,7 +18,9 @@ BENCHLIB  := $(LIBDIR)/libmchecksum_bench.so
 COBJS     := $(BUILD)/mchecksum_cpu.o $(BUILD)/mchecksum_models.o $(BUILD)/crc_tables.o
 GOBJS     := $(BUILD)/mchecksum_gpu.o $(BUILD)/mchecksum_gpu_ext.o
 
-all: $(LIB) $(BENCHLIB) oracle $(BUILD)/c1_bench
+QFAULTLIB := $(BUILD)/libmchecksum_qfault.so
+
+all: $(LIB) $(BENCHLIB) oracle $(BUILD)/c1_bench $(QFAULTLIB)
 
 $(BUILD) $(LIBDIR):
 	mkdir -p $@
@@ -38,6 +40,15 @@ $(BUILD)/bench_datagen.o: $(CSRC)/bench_datagen.hip | $(BUILD)
 $(LIB): $(COBJS) $(GOBJS) | $(LIBDIR)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^ -lpthread -Wl,-soname,libmchecksum.so.2
 	ln -sf libmchecksum.so $(LIBDIR)/libmchecksum.so.2
+
+# Test-only build: the work queue gives up one wait per launch
+# (MCK_QFAULT_TEST, crc_gpu_device.h), loaded by tests/test_gpu_fail_closed.py
+# next to the product library to check that such a launch fails closed.
+$(BUILD)/qfault_gpu.o: $(CSRC)/mchecksum_gpu.hip $(wildcard $(CSRC)/*.h) include/mchecksum_gpu.h | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -DMCK_QFAULT_TEST=1 $(INC) -c $< -o $@
+
+$(QFAULTLIB): $(COBJS) $(BUILD)/qfault_gpu.o $(BUILD)/mchecksum_gpu_ext.o
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^ -lpthread
 
 $(BENCHLIB): $(BUILD)/bench_datagen.o | $(LIBDIR)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^

@@ -24,9 +24,19 @@
  *
  * Streams: `stream` is a hipStream_t (NULL = the default stream).  Calls are
  * asynchronous and capture-safe once mchecksum_gpu_prepare() has run for the
- * method on the current device (it uploads the lookup tables).  Up to 3072
- * calls may be in flight at once per device; each captured call keeps a
- * device-side work-queue slot of its own for every replay, 1024 per device.
+ * method on the current device (it uploads the lookup tables).  Large batches
+ * balance their payloads through a device-side work-queue slot: eager calls
+ * cycle through 3072 slots per device, captured calls through 1024 (a captured
+ * call keeps its slot for every replay).  Slots are claimed by the running
+ * launch, so launches that meet on one slot (more than 3072 calls in flight,
+ * or two graph execs of one capture replayed at the same time) still hash
+ * every payload: the later one takes a static split of the batch instead.
+ *
+ * Fail closed: every wait in the work queue is bounded.  A launch in which a
+ * wait gives up (a protocol fault; 0 in every test run) adds 1 to the error
+ * word set with mchecksum_gpu_set_error_word(), adds `count` to the mismatch
+ * counter of a verify call and marks every payload it cannot vouch for with
+ * status 1, so unhashed bytes never read as verified.
  *
  * There is NO host fallback: without a usable HIP device every call returns
  * MCHECKSUM_GPU_ENODEV.
@@ -146,6 +156,15 @@ mchecksum_gpu_verify_core_headers(const char *hash_method, int kind,
  * this length (1..64), for reporting; -1 on error. */
 MCHECKSUM_PUBLIC int
 mchecksum_gpu_lanes_per_payload(const char *hash_method, size_t len);
+
+/* Fail-closed report for the batch calls this host thread makes from now on:
+ * each call whose launch could not hash every payload adds 1 to *dev_word
+ * (a device-resident uint32_t the caller owns, zeroes and reads after the
+ * calls' streams are synchronized).  The word is captured by value into
+ * graph-captured calls.  NULL (the default) turns the report off; the
+ * process-wide count mchecksum_gpu_queue_faults() is always kept. */
+MCHECKSUM_PUBLIC int
+mchecksum_gpu_set_error_word(uint32_t *dev_word);
 
 /* Human-readable text for the last error on this thread. */
 MCHECKSUM_PUBLIC const char *

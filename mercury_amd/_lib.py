@@ -23,7 +23,7 @@ GPU_SYMBOLS = ("mchecksum_gpu_available", "mchecksum_gpu_prepare", "mchecksum_gp
                "mchecksum_gpu_checksum_offsets", "mchecksum_gpu_verify_offsets", "mchecksum_gpu_verify_messages",
                "mchecksum_gpu_lanes_per_payload", "mchecksum_gpu_last_error", "mchecksum_gpu_segments_work_size",
                "mchecksum_gpu_checksum_segments", "mchecksum_gpu_verify_core_headers",
-               "mchecksum_gpu_queue_faults")
+               "mchecksum_gpu_queue_faults", "mchecksum_gpu_set_error_word")
 CORE_HEADER_REQUEST, CORE_HEADER_RESPONSE = 0, 1
 
 _lib = None
@@ -80,6 +80,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     L.mchecksum_gpu_last_error.restype = c_char_p
     L.mchecksum_gpu_queue_faults.argtypes = []
     L.mchecksum_gpu_queue_faults.restype = ctypes.c_longlong
+    L.mchecksum_gpu_set_error_word.argtypes = [c_void_p]
+    L.mchecksum_gpu_set_error_word.restype = c_int
     _lib = L
     return L
 

@@ -156,6 +156,12 @@ struct BatchArgs {
     uint32_t msg, pay_off, hash_off;
     // work-queue slot (WgQueue below); nullptr = static assignment
     unsigned long long *queue;
+    // 1: claim the slot's owner word (slots the host cannot hand out
+    // exclusively: graph-captured launches and overflow streams)
+    uint32_t own;
+    // optional caller word (mchecksum_gpu_set_error_word): +1 when this launch
+    // could not hash every payload (fail-closed report for checksum modes)
+    uint32_t *err_word;
 };
 
 // ------------------------------------------------------------ work queue --
@@ -182,12 +188,33 @@ struct BatchArgs {
 // a slot from a ring, mchecksum_gpu.hip).  tests/test_queue_model.py runs the
 // same protocol on the CPU under random interleavings.
 // Slot layout (one counter per 256-B line): [0, 8) sub-queue tickets,
-// [8, 16) exited workgroups per group (blockIdx % 8), [16] exited groups.
+// [8, 16) exited workgroups per group (blockIdx % 8), [16] exited groups,
+// [17] fault flag of the launch, [18] owner tag.
+//
+// Ownership.  A slot must only ever be used by one launch at a time.  The
+// host gives every stream a slot of its own (launches on one stream never
+// overlap), so eager launches need no check.  Where the host cannot promise
+// exclusivity -- a graph-captured launch keeps its slot for every replay, and
+// two graph execs of one capture may replay at the same time; streams beyond
+// the per-stream table share hashed slots -- the launch runs with own = 1:
+// every workgroup's first thread reads the owner word and, while it is 0,
+// claims it with a CAS of the launch's tag (its kernarg address -- distinct
+// for any two launches that run at the same time); the last group releases
+// it, owner word last.  (Same-address reads and CASes from 256 workgroups
+// serialise at one L2 channel: ~0.5% of the headline launch, so eager
+// launches skip it.)  A workgroup that finds the slot owned by another launch
+// never touches it and takes the static split instead (units wave,
+// wave + #waves, ...): every unit is still hashed, at the static split's speed.  (If some workgroups of one launch see the slot busy and
+// later ones see it free, the static ones repeat units the queue also hands
+// out: CRCs are written twice with the same value; verify mismatch counts may
+// then over-count, never under-count.)
 constexpr uint32_t kQSub = 8;
 constexpr uint32_t kQStride = 32;  // u64 words between counters
 constexpr uint32_t kQGroupDone = kQSub;
 constexpr uint32_t kQAllDone = 2 * kQSub;
-constexpr uint32_t kQSlotWords = (2 * kQSub + 1) * kQStride;
+constexpr uint32_t kQFault = 2 * kQSub + 1;
+constexpr uint32_t kQOwner = 2 * kQSub + 2;
+constexpr uint32_t kQSlotWords = (2 * kQSub + 3) * kQStride;
 // Chunk size: a power of two, about a quarter of a workgroup's fair share
 // of units, between 1 and 32 (C4: 32 units; a 5000-payload batch: 4).
 // Fixed 16 starved half the workgroups of C3's 8192 units at 2 WGs per CU; 32
@@ -252,6 +279,7 @@ struct WgQueue {
     unsigned int slot;     // next (chunk, unit) slot of this workgroup
     unsigned int drained;  // sub-queues (counted from home) found empty
     unsigned int exited;   // waves of this workgroup that left the loop
+    unsigned int busy;     // 1: the slot belongs to another launch -> static split
     unsigned int reads[kWgRing];
     unsigned long long entry[kWgRing];  // (chunk seq << 32) | global chunk id
 };
@@ -329,42 +357,84 @@ __device__ uint64_t wg_fetch(WgQueue *L, unsigned long long *q, uint64_t nch) {
     return kNoChunk;
 }
 
-// One lane: make chunk `seq` of this workgroup known in the ring.
-__device__ void wg_publish(WgQueue *L, uint32_t seq, uint64_t id, uint32_t cl) {
+// One lane: make chunk `seq` of this workgroup known in the ring.  Returns
+// false when the wait for the ring entry's readers gave up (fault counted).
+__device__ bool wg_publish(WgQueue *L, uint32_t seq, uint64_t id, uint32_t cl) {
     const uint32_t r = seq % kWgRing;
+    bool ok = true;
     uint32_t spins = 0;
     (void)spins;
     if (seq >= kWgRing)
         while (lds_ld(&L->reads[r]) != (1u << cl)) {
             __builtin_amdgcn_s_sleep(1);
-            MCK_SPIN_GUARD(spins, 1, seq, lds_ld(&L->reads[r]))
+            if (++spins > kSpinMax) {
+                queue_fault(1, seq, lds_ld(&L->reads[r]));
+                ok = false;
+                break;
+            }
         }
     lds_st(&L->reads[r], 0u);
     lds_st(&L->entry[r], (unsigned long long)seq << 32 | id);
+    return ok;
 }
 
-// Thread 0, before the kernel's first barrier: reset the LDS state and
-// publish the first chunk (its fetch overlaps the LDS table fill).
-__device__ __attribute__((unused)) void wg_queue_init(WgQueue *L, unsigned long long *q, uint64_t n) {
+// The launch's tag: its kernarg segment address.  Two launches that run at
+// the same time never share one (each reads its own arguments while it runs).
+__device__ __forceinline__ unsigned long long launch_tag() {
+    return reinterpret_cast<uint64_t>(__builtin_amdgcn_kernarg_segment_ptr());
+}
+
+// Thread 0, before the kernel's first barrier: reset the LDS state, claim the
+// slot for this launch when the host asks for it (own: see "Ownership") and
+// publish the first chunk (its fetch overlaps the LDS table fill).  A slot
+// owned by another launch is left alone: the workgroup then takes the static
+// split (busy = 1).
+__device__ __attribute__((unused)) void wg_queue_init(WgQueue *L, unsigned long long *q, uint64_t n, bool own) {
     L->slot = 0;
     L->drained = 0;
     L->exited = 0;
+    L->busy = 0;
     for (uint32_t r = 0; r < kWgRing; r++) {
         L->reads[r] = 0;
         L->entry[r] = ~0ull;
     }
+    if (own) {
+        unsigned long long *ow = q + kQOwner * kQStride;
+        const unsigned long long tag = launch_tag();
+        unsigned long long owner = __hip_atomic_load(ow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (owner == 0ull) owner = atomicCAS(ow, 0ull, tag);
+        if (owner != 0ull && owner != tag) {
+            L->busy = 1;
+            return;
+        }
+    }
     const ChunkPlan plan(n);
-    wg_publish(L, 0, wg_fetch(L, q, plan.nch), plan.cl);
+    (void)wg_publish(L, 0, wg_fetch(L, q, plan.nch), plan.cl);
 }
 
 // Calls body(u) for this wave's units: through the work queue (DYN: the
 // throughput kernels; the host always passes a slot, wg_queue_init has run)
-// or u = wave, wave + nw, ... (the light layout's small batches).  One path
-// per kernel: both in one kernel cost the register-tight CRC-64 loops spills.
+// or u = wave, wave + nw, ... (the light layout's small batches, and a DYN
+// workgroup whose slot belongs to another launch).
+//
+// Fail closed.  Every wait of the queue protocol is bounded; a wave whose wait
+// gives up leaves the loop, and the units it would still have taken may then
+// never be hashed.  for_each_unit returns true in the FIRST such wave of the
+// launch (one fault flag per slot), which must then run fail_closed(): it
+// reports the launch as failed, so unhashed bytes never read as verified.
+// -DMCK_QFAULT_TEST=1 (test builds only) forces one give-up per launch.
+#ifndef MCK_QFAULT_TEST
+#define MCK_QFAULT_TEST 0
+#endif
 template <bool DYN, class F>
-__device__ __forceinline__ void for_each_unit(WgQueue *L, unsigned long long *queue, uint64_t n, uint32_t wave,
-                                              uint32_t nw, F &&body) {
+__device__ __forceinline__ bool for_each_unit(WgQueue *L, unsigned long long *queue, uint64_t n, uint32_t wave,
+                                              uint32_t nw, bool own, F &&body) {
     if constexpr (DYN) {
+        // One call site of body for both splits: a second inlined copy of the
+        // payload loop made the offsets kernels spill, and so does the copy
+        // loop unswitching makes -- hence busy is re-read from LDS every
+        // iteration (an atomic load the compiler cannot hoist).
+        uint64_t su = wave;  // static cursor (busy slot)
         const bool l0 = (threadIdx.x & 63u) == 0;
 #ifndef MCK_QLEAD_DIV
 #define MCK_QLEAD_DIV 4
@@ -377,54 +447,78 @@ __device__ __forceinline__ void for_each_unit(WgQueue *L, unsigned long long *qu
 #endif
         const uint64_t max_iters = (uint64_t)cu * nch + 4ull * cu + 64;
         uint64_t iters = 0;
+        uint32_t flt = 0;  // lane 0: a wait of this wave gave up
         for (;;) {
-            uint64_t e = 0;
-            uint32_t t = 0;
-            if (++iters > max_iters) {  // more slots than the launch has: protocol fault
-                if (l0) queue_fault(3, iters, 0);
-                break;
-            }
-            if (l0) {
-                t = atomicAdd(&L->slot, 1u);
-                const uint32_t seq = t >> cl, r = seq % kWgRing;
-                uint32_t spins = 0;
-                (void)spins;
-#if MCK_TRACE
-                const unsigned long long w0 = wall_clock64();
-                unsigned long long f0 = 0;
-#endif
-                while (((e = lds_ld(&L->entry[r])) >> 32) != seq) {
-                    __builtin_amdgcn_s_sleep(1);
-                    MCK_SPIN_GUARD(spins, 2, seq, e)
+            uint64_t u;
+            if (__builtin_amdgcn_readfirstlane(lds_ld(&L->busy))) {
+                if (su >= n) break;
+                u = su;
+                su += nw;
+            } else {
+                uint64_t e = 0;
+                uint32_t t = 0;
+                if (++iters > max_iters) {  // more slots than the launch has: protocol fault
+                    if (l0) {
+                        queue_fault(3, iters, 0);
+                        flt = 1;
+                    }
+                    break;
                 }
+                if (l0) {
+                    t = atomicAdd(&L->slot, 1u);
+                    const uint32_t seq = t >> cl, r = seq % kWgRing;
+                    uint32_t spins = 0;
+                    (void)spins;
 #if MCK_TRACE
-                qs_wait += wall_clock64() - w0;
+                    const unsigned long long w0 = wall_clock64();
+                    unsigned long long f0 = 0;
 #endif
-                if ((e >> 32) != seq) e = kNoChunk;  // gave up (fault counted)
-                atomicAdd(&L->reads[r], 1u);
-                // One taker per chunk (slot cu - lead) fetches the next
-                // chunk -- after its own chunk is known, so fetches run in chunk
-                // order and the first kNoChunk is final.
-                if ((t & (cu - 1)) == cu - lead) {
+                    while (((e = lds_ld(&L->entry[r])) >> 32) != seq) {
+                        __builtin_amdgcn_s_sleep(1);
+                        MCK_SPIN_GUARD(spins, 2, seq, e)
+                    }
 #if MCK_TRACE
-                    f0 = wall_clock64();
+                    qs_wait += wall_clock64() - w0;
 #endif
-                    const uint64_t nid = (e & 0xFFFFFFFFull) == kNoChunk ? kNoChunk : wg_fetch(L, queue, nch);
+                    if ((e >> 32) != seq) {  // gave up (fault counted)
+                        e = kNoChunk;
+                        flt = 1;
+                    }
+                    atomicAdd(&L->reads[r], 1u);
+                    // One taker per chunk (slot cu - lead) fetches the next
+                    // chunk -- after its own chunk is known, so fetches run in
+                    // chunk order and the first kNoChunk is final.
+                    if ((t & (cu - 1)) == cu - lead) {
 #if MCK_TRACE
-                    const unsigned long long df = wall_clock64() - f0;
-                    qs_n++;
-                    qs_sum += df;
-                    qs_max = df > qs_max ? df : qs_max;
+                        f0 = wall_clock64();
 #endif
-                    wg_publish(L, seq + 1, nid, cl);
+                        const uint64_t nid = (e & 0xFFFFFFFFull) == kNoChunk ? kNoChunk : wg_fetch(L, queue, nch);
+#if MCK_TRACE
+                        const unsigned long long df = wall_clock64() - f0;
+                        qs_n++;
+                        qs_sum += df;
+                        qs_max = df > qs_max ? df : qs_max;
+#endif
+                        if (!wg_publish(L, seq + 1, nid, cl)) flt = 1;
+                    }
+#if MCK_QFAULT_TEST
+                    // injected give-up: workgroup 3 drops the first unit of its
+                    // second chunk (after its reads/publish duties, so the rest
+                    // of the launch runs on)
+                    if (blockIdx.x == 3 && seq == 1 && (t & (cu - 1)) == 0 && !flt) {
+                        queue_fault(9, seq, t);
+                        e = kNoChunk;
+                        flt = 1;
+                    }
+#endif
                 }
+                t = __builtin_amdgcn_readfirstlane(t);
+                const uint64_t id = uniform64(e) & 0xFFFFFFFFull;
+                if (id == kNoChunk) break;
+                // every chunk spans cu slots; a tail chunk's slots past its size are skipped
+                const uint32_t k = t & (cu - 1);
+                u = k < plan.size(id) ? plan.start(id) + k : n;
             }
-            t = __builtin_amdgcn_readfirstlane(t);
-            const uint64_t id = uniform64(e) & 0xFFFFFFFFull;
-            if (id == kNoChunk) break;
-            // every chunk spans cu slots; a tail chunk's slots past its size are skipped
-            const uint32_t k = t & (cu - 1);
-            const uint64_t u = k < plan.size(id) ? plan.start(id) + k : n;
 #if MCK_TRACE
             const unsigned long long b0 = wall_clock64();
 #endif
@@ -445,23 +539,57 @@ __device__ __forceinline__ void for_each_unit(WgQueue *L, unsigned long long *qu
             g_mck_qwave[4 * 16384 + 2 * wave + 1] = qs_busy;
         }
 #endif
+        if (__builtin_amdgcn_readfirstlane(lds_ld(&L->busy))) return false;  // never touched the slot
+        // The first faulting wave of the launch claims the slot's fault flag
+        // (before its own exit is counted, so the slot cannot be released yet).
+        uint32_t first = 0;
+        if (l0 && flt) first = atomicCAS(queue + kQFault * kQStride, 0ull, 1ull) == 0ull;
         // Exit counting is hierarchical: one global atomic per wave on a
         // single line serialised ~4096 x 45 ns at the end of every launch
         // (C2 ran 2x slower).  Waves count in LDS, the last wave of a
         // workgroup counts in its group's line, the last workgroup of a group
-        // in the slot's line; the last group zeroes the slot.
+        // in the slot's line; the last group zeroes the slot and releases it,
+        // the owner word last (after every other zero has reached L2).
+        uint32_t last = 0;
         if (l0 && atomicAdd(&L->exited, 1u) == blockDim.x / 64u - 1u) {
             const uint32_t g = blockIdx.x % kQSub;
             const uint32_t wgs = (gridDim.x - g + kQSub - 1) / kQSub;  // workgroups in group g
             const uint32_t groups = gridDim.x < kQSub ? gridDim.x : kQSub;
-            if (atomicAdd(queue + (kQGroupDone + g) * kQStride, 1ull) == wgs - 1ull &&
-                atomicAdd(queue + kQAllDone * kQStride, 1ull) == groups - 1ull)
-                for (uint32_t j = 0; j <= kQAllDone; j++) atomicExch(queue + j * kQStride, 0ull);
+            last = atomicAdd(queue + (kQGroupDone + g) * kQStride, 1ull) == wgs - 1ull &&
+                   atomicAdd(queue + kQAllDone * kQStride, 1ull) == groups - 1ull;
+        }
+        if (__builtin_amdgcn_readfirstlane(last)) {  // one instruction: lane j zeroes line j
+            const uint32_t j = threadIdx.x & 63u;
+            if (j < kQOwner) atomicExch(queue + j * kQStride, 0ull);
+            if (own) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (j == 0) atomicExch(queue + kQOwner * kQStride, 0ull);
+            }
         }
         (void)nw;
+        return __builtin_amdgcn_readfirstlane(first) != 0;
     } else {
+        (void)own;
         for (uint64_t u = wave; u < n; u += nw) body(u);
+        return false;
     }
+}
+
+// Run by the wave for_each_unit picked after a give-up (wave-uniform): the
+// launch did not hash every payload, so it must not read as clean.  The
+// caller's error word (if set) gets +1; a verify launch adds `count` to the
+// mismatch counter and marks every payload's status 1 -- payloads that are
+// hashed after this sweep overwrite theirs with the true result, so each
+// status ends as the correct value or 1 ("flagged"), never a stale 0.
+template <bool VERIFY>
+__device__ __forceinline__ void fail_closed(const BatchArgs &a) {
+    const uint32_t lane = threadIdx.x & 63u;
+    if (lane == 0) {
+        if (a.err_word) atomicAdd(a.err_word, 1u);
+        if (VERIFY && a.mismatches) atomicAdd(a.mismatches, (uint32_t)a.count);
+    }
+    if (VERIFY && a.status)
+        for (uint64_t p = lane; p < a.count; p += 64) a.status[p] = 1;
 }
 
 // Network-order u32 at an arbitrary byte address (the HG header's payload
@@ -593,7 +721,7 @@ __device__ void fill_lds32(uint8_t *lds, const crc32_gpu_pack_t *pk) {
 #define MCK_ALIGNED32_V2 1
 #endif
 #ifndef MCK_LA32
-#define MCK_LA32 0
+#define MCK_LA32 1
 #endif
 // Global-address-space views: loads through them are global_load (never
 // flat_load, which would also count against lgkmcnt and make every LDS wait
@@ -913,7 +1041,7 @@ __global__ __launch_bounds__(kBlk32<LIGHT>, 1) void crc32c_batch_kernel(BatchArg
 #if defined(MCK_EMPTY) && MCK_EMPTY == 2
     if (!DYN) return;  // diagnostic: launch cost alone
 #endif
-    if (DYN && threadIdx.x == 0) wg_queue_init(&wgq, a.queue, units);
+    if (DYN && threadIdx.x == 0) wg_queue_init(&wgq, a.queue, units, a.own);
     fill_lds32<LIGHT, kBlk32<LIGHT>>(lds_raw, pk);
     __syncthreads();
 #if defined(MCK_EMPTY) && MCK_EMPTY == 1
@@ -949,7 +1077,7 @@ __global__ __launch_bounds__(kBlk32<LIGHT>, 1) void crc32c_batch_kernel(BatchArg
             }
         };
         if constexpr (!LIGHT) {
-            for_each_unit<true>(&wgq, a.queue, units, wave, nw, one);
+            if (for_each_unit<true>(&wgq, a.queue, units, wave, nw, a.own, one)) fail_closed<VERIFY>(a);
         } else {  // static: a byte-balanced contiguous range per wave
             uint64_t first, last;
             wave_range(a.offsets, a.count, wave, nw, &first, &last);
@@ -958,7 +1086,7 @@ __global__ __launch_bounds__(kBlk32<LIGHT>, 1) void crc32c_batch_kernel(BatchArg
         MCK_STAMP(wave, 2);
         return;
     }
-    for_each_unit<DYN>(&wgq, a.queue, units, wave, nw, [&](uint64_t u) {
+    const bool faulted = for_each_unit<DYN>(&wgq, a.queue, units, wave, nw, a.own, [&](uint64_t u) {
         const uint64_t p = u * PPW + grp;
         const bool act = p < a.count;
         const uint64_t pc = act ? p : a.count - 1;
@@ -969,6 +1097,7 @@ __global__ __launch_bounds__(kBlk32<LIGHT>, 1) void crc32c_batch_kernel(BatchArg
             x = payload32_generic<LOG2G, NT>(lds, pk, a.base + pc * a.stride, a.len, gl, lc0, lc1);
         if (act && gl == 0) emit<uint32_t, VERIFY>(a, p, x ^ xorout);
     });
+    if (faulted) fail_closed<VERIFY>(a);
     MCK_STAMP(wave, 2);
 }
 
@@ -1370,7 +1499,7 @@ __global__ __launch_bounds__(kBlk64<MODE>, kWpe64<MODE>) void crc64_batch_kernel
     const uint64_t units = MODE == kOffsets ? a.count : (a.count + PPW - 1) / PPW;
     __shared__ WgQueue wgq;
     constexpr bool DYN = dyn_policy(64, MODE, NT, false);
-    if (DYN && threadIdx.x == 0) wg_queue_init(&wgq, a.queue, units);
+    if (DYN && threadIdx.x == 0) wg_queue_init(&wgq, a.queue, units, a.own);
     fill_lds64<S::block, S::ops_mode>(lds, pk);
     __syncthreads();
 
@@ -1395,10 +1524,10 @@ __global__ __launch_bounds__(kBlk64<MODE>, kWpe64<MODE>) void crc64_batch_kernel
                                                 : payload64_generic<LOG2G, NT, S::ops_mode>(lds, pk, a.base + o, n, gl, lc);
             if (gl == 0) emit<uint64_t, VERIFY>(a, p, x ^ xorout);
         };
-        for_each_unit<true>(&wgq, a.queue, units, wave, nw, one);
+        if (for_each_unit<true>(&wgq, a.queue, units, wave, nw, a.own, one)) fail_closed<VERIFY>(a);
         return;
     }
-    for_each_unit<DYN>(&wgq, a.queue, units, wave, nw, [&](uint64_t u) {
+    const bool faulted = for_each_unit<DYN>(&wgq, a.queue, units, wave, nw, a.own, [&](uint64_t u) {
         const uint64_t p = u * PPW + grp;
         const bool act = p < a.count;
         const uint64_t pc = act ? p : a.count - 1;
@@ -1409,6 +1538,7 @@ __global__ __launch_bounds__(kBlk64<MODE>, kWpe64<MODE>) void crc64_batch_kernel
             x = payload64_generic<LOG2G, NT>(lds, pk, a.base + pc * a.stride, a.len, gl, lc);
         if (act && gl == 0) emit<uint64_t, VERIFY>(a, p, x ^ xorout);
     });
+    if (faulted) fail_closed<VERIFY>(a);
 }
 
 }  // namespace

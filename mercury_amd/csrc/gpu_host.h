@@ -8,6 +8,7 @@
 
 #include <cstdint>
 #include <mutex>
+#include <unordered_map>
 
 #include "crc_gpu_device.h"
 #include "mchecksum_models.h"
@@ -22,19 +23,23 @@ struct DevCtx {
     void *pack[MCK_NMODELS][CRC_GPU_MAX_LOG2G + 1] = {};
     void *ext[MCK_NMODELS] = {};  // mchecksum_gpu_ext.hip's per-model tables
     // Work-queue slots of the batch kernels (WgQueue, crc_gpu_device.h):
-    // kQueueSlots zeroed counter sets; a launch's last wave re-zeroes its slot.
-    // Eager launches take the next slot of a ring of kEagerSlots, so launches
-    // that run at the same time (different streams) get different slots unless
-    // more than kEagerSlots are in flight at once.  A launch captured into a
-    // hipGraph keeps its slot for every replay, so it gets one of its own from
-    // the remaining kCapturedSlots, never handed out again.
+    // kQueueSlots zeroed counter sets; a launch's last group re-zeroes its slot.
+    // Eager launches use a slot of their stream's own (the first kStreamSlots
+    // streams seen on the device; launches on one stream never overlap).  A
+    // launch captured into a hipGraph keeps its slot for every replay: those
+    // come round-robin from kCapturedSlots; streams past the table share
+    // kOverflowSlots by hash.  Both of those claim the slot on the device
+    // (BatchArgs::own) and a launch that finds it owned by another running
+    // launch takes the static split (crc_gpu_device.h, "Ownership"), so a
+    // collision costs speed, never correctness.
     unsigned long long *queue = nullptr;
-    uint32_t queue_next = 0;
     uint32_t queue_captured = 0;
+    std::unordered_map<void *, uint32_t> stream_slot;  // guarded by g_mu
 };
-constexpr uint32_t kQueueSlots = 4096;
+constexpr uint32_t kStreamSlots = 2048;
 constexpr uint32_t kCapturedSlots = 1024;
-constexpr uint32_t kEagerSlots = kQueueSlots - kCapturedSlots;
+constexpr uint32_t kOverflowSlots = 1024;
+constexpr uint32_t kQueueSlots = kStreamSlots + kCapturedSlots + kOverflowSlots;
 
 extern std::mutex g_mu;
 
@@ -48,8 +53,8 @@ int device_ctx(DevCtx **out);
 // Model + device context + table pack for lanes-per-payload 2^log2g (takes g_mu).
 int prologue(const char *method, int log2g, int *width, DevCtx **c, const void **pack);
 // Work-queue slot for one launch of a throughput (non-light) batch kernel on
-// `stream`; nullptr (error recorded) once a device's captured slots run out.
-unsigned long long *queue_slot(DevCtx *c, void *stream);
+// `stream`; *own = 1 when the launch must claim it on the device.
+unsigned long long *queue_slot(DevCtx *c, void *stream, uint32_t *own);
 
 }  // namespace mck
 

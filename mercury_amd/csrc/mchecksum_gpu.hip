@@ -48,6 +48,9 @@ namespace mck {
 // ------------------------------------------------------------ host side ----
 
 thread_local char t_err[256] = "";
+// mchecksum_gpu_set_error_word(): device word bumped by a launch that could
+// not hash every payload (per host thread; nullptr = none)
+thread_local uint32_t *t_err_word = nullptr;
 
 int set_err(int rc, const char *fmt, ...) {
     va_list ap;
@@ -141,22 +144,39 @@ int get_pack(DevCtx *c, int idx, int log2g, const void **pack) {
     return 0;
 }
 
-unsigned long long *queue_slot(DevCtx *c, void *stream) {
+unsigned long long *queue_slot(DevCtx *c, void *stream, uint32_t *own) {
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing((hipStream_t)stream, &st) != hipSuccess) {
         (void)hipGetLastError();
         st = hipStreamCaptureStatusNone;
     }
     if (st == hipStreamCaptureStatusActive) {
-        const uint32_t k = __atomic_fetch_add(&c->queue_captured, 1u, __ATOMIC_RELAXED);
-        if (k >= kCapturedSlots) {
-            set_err(MCHECKSUM_GPU_EINVAL, "more than %u graph-captured queue launches on this device", kCapturedSlots);
-            return nullptr;
-        }
-        return c->queue + (size_t)(kEagerSlots + k) * kQSlotWords;
+        // Captured launches keep their slot for every replay, round-robin over
+        // the captured range; the kernel claims it (two replays that meet on
+        // one slot stay correct: the later one takes the static split).
+        // (MCHECKSUM_GPU_CAPTURED_SLOTS=n, tests only: use n captured slots)
+        static const uint32_t ncap = [] {
+            const char *e = getenv("MCHECKSUM_GPU_CAPTURED_SLOTS");
+            const long v = e && e[0] ? atol(e) : 0;
+            return v >= 1 && v <= (long)kCapturedSlots ? (uint32_t)v : kCapturedSlots;
+        }();
+        const uint32_t k = __atomic_fetch_add(&c->queue_captured, 1u, __ATOMIC_RELAXED) % ncap;
+        *own = 1;
+        return c->queue + (size_t)(kStreamSlots + k) * kQSlotWords;
     }
-    const uint32_t s = __atomic_fetch_add(&c->queue_next, 1u, __ATOMIC_RELAXED) % kEagerSlots;
-    return c->queue + (size_t)s * kQSlotWords;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        auto it = c->stream_slot.find(stream);
+        if (it == c->stream_slot.end() && c->stream_slot.size() < kStreamSlots)
+            it = c->stream_slot.emplace(stream, (uint32_t)c->stream_slot.size()).first;
+        if (it != c->stream_slot.end()) {
+            *own = 0;  // this stream's own slot: its launches never overlap
+            return c->queue + (size_t)it->second * kQSlotWords;
+        }
+    }
+    const uint64_t h = ((uint64_t)(uintptr_t)stream >> 4) * 0x9E3779B97F4A7C15ull;
+    *own = 1;
+    return c->queue + (size_t)(kStreamSlots + kCapturedSlots + (uint32_t)((h >> 32) % kOverflowSlots)) * kQSlotWords;
 }
 
 typedef void (*kern_t)(BatchArgs);
@@ -297,6 +317,7 @@ int do_offsets(const char *method, const void *base, const uint64_t *offsets, si
     a.pay_off = (uint32_t)pay_off;
     a.hash_off = (uint32_t)hash_off;
     a.queue = nullptr;
+    a.err_word = t_err_word;
     if (msg && width != 32)
         return set_err(MCHECKSUM_GPU_EMETHOD, "message verify carries a 32-bit header hash: crc32c only");
     KLaunch k;
@@ -314,7 +335,7 @@ int do_offsets(const char *method, const void *base, const uint64_t *offsets, si
     else
         k = verify ? (nt ? kernel_ptr<64, 6, kOffsets, true, true>() : kernel_ptr<64, 6, kOffsets, true>())
                    : (nt ? kernel_ptr<64, 6, kOffsets, false, true>() : kernel_ptr<64, 6, kOffsets, false>());
-    if (dyn_policy(width, kOffsets, nt, light) && !(a.queue = queue_slot(c, stream))) return MCHECKSUM_GPU_EINVAL;
+    if (dyn_policy(width, kOffsets, nt, light)) a.queue = queue_slot(c, stream, &a.own);
     return launch(k, a, grid_for(c, count, k), stream);
 }
 
@@ -332,11 +353,11 @@ int launch_fixed(DevCtx *c, const void *pack, int width, int lg, const void *dev
     a.count = count;
     a.out = dev_out;
     a.pack = pack;
+    a.err_word = t_err_word;
     const bool nt = !light && use_nt((uint64_t)len * count);
     const KLaunch k = width == 32 ? pick_fixed<32>(lg, aligned, nt, light) : pick_fixed<64>(lg, aligned, nt, false);
     const uint64_t ppw = 64u >> lg;
-    if (dyn_policy(width, aligned ? kFixedAligned : kFixedGeneric, nt, light) && !(a.queue = queue_slot(c, stream)))
-        return MCHECKSUM_GPU_EINVAL;
+    if (dyn_policy(width, aligned ? kFixedAligned : kFixedGeneric, nt, light)) a.queue = queue_slot(c, stream, &a.own);
     const uint64_t units = (count + ppw - 1) / ppw;
     unsigned blocks = grid_for(c, units, k);
     // CRC-64 static split with fewer units than one full workgroup per CU:
@@ -436,6 +457,11 @@ int mchecksum_gpu_verify_messages(const char *hash_method, const void *dev_buf, 
 }
 
 const char *mchecksum_gpu_last_error(void) { return t_err; }
+
+int mchecksum_gpu_set_error_word(uint32_t *dev_word) {
+    t_err_word = dev_word;
+    return MCHECKSUM_GPU_OK;
+}
 
 long long mchecksum_gpu_queue_faults(void) {
     if (!mchecksum_gpu_available()) return -1;

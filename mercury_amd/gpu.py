@@ -35,12 +35,30 @@ def out_dtype(method: str) -> torch.dtype:
     return torch.int32 if w == 4 else torch.int64
 
 
-def _stream_handle(stream) -> int:
+def _stream_handle(stream, device=None) -> int:
+    """hipStream_t for a call on `device` (the data tensor's device): None =
+    that device's current stream; a torch stream must belong to it."""
     if stream is None:
-        return torch.cuda.current_stream().cuda_stream
+        return torch.cuda.current_stream(device).cuda_stream
     if hasattr(stream, "cuda_stream"):
+        if device is not None and getattr(stream, "device", device) != device:
+            raise GpuChecksumError(f"stream belongs to {stream.device}, data to {device}")
         return stream.cuda_stream
     return int(stream)
+
+
+def _same_device(data: torch.Tensor, **tensors):
+    """Every tensor argument must live on data's device: the library launches
+    on the current device, which _on(data) makes data's."""
+    for name, t in tensors.items():
+        if t is not None and (not isinstance(t, torch.Tensor) or t.device != data.device):
+            raise GpuChecksumError(f"{name} must be a tensor on {data.device}")
+
+
+def _on(data: torch.Tensor):
+    """Make data's device current for the call (the C library picks its table
+    pack and queue slot from hipGetDevice())."""
+    return torch.cuda.device(data.device)
 
 
 def _check_device_u8(t: torch.Tensor, name: str):
@@ -59,6 +77,16 @@ def queue_faults() -> int:
     device since load (bounded waits that gave up; 0 when healthy).
     Synchronizes the device."""
     return int(_lib().mchecksum_gpu_queue_faults())
+
+
+def set_error_word(word: torch.Tensor | None) -> None:
+    """Fail-closed report (mchecksum_gpu_set_error_word): every later batch call
+    of this host thread adds 1 to `word` (a one-element device int32 tensor the
+    caller zeroes) when its launch could not hash every payload.  None turns
+    the report off.  Keep the tensor alive while it is set."""
+    if word is not None and (word.dtype != torch.int32 or not word.is_cuda or word.numel() < 1):
+        raise GpuChecksumError("error word must be a device int32 tensor")
+    _lib().mchecksum_gpu_set_error_word(word.data_ptr() if word is not None else None)
 
 
 def prepare(method: str = "crc32c") -> None:
@@ -90,8 +118,10 @@ def checksum_fixed(method: str, data: torch.Tensor, length: int, count: int | No
         out = torch.empty(count, dtype=out_dtype(method), device=data.device)
     elif out.numel() < count or out.dtype != out_dtype(method) or not out.is_cuda:
         raise GpuChecksumError("out tensor has the wrong size, dtype or device")
-    rc = _lib().mchecksum_gpu_checksum_fixed(method.encode(), data.data_ptr(), stride, length, count,
-                                             out.data_ptr(), _stream_handle(stream))
+    _same_device(data, out=out)
+    with _on(data):
+        rc = _lib().mchecksum_gpu_checksum_fixed(method.encode(), data.data_ptr(), stride, length, count,
+                                                 out.data_ptr(), _stream_handle(stream, data.device))
     if rc != 0:
         _err(rc, "mchecksum_gpu_checksum_fixed")
     return out
@@ -125,8 +155,10 @@ def checksum_offsets(method: str, data: torch.Tensor, offsets: torch.Tensor, out
         out = torch.empty(count, dtype=out_dtype(method), device=data.device)
     elif out.numel() < count or out.dtype != out_dtype(method) or not out.is_cuda:
         raise GpuChecksumError("out tensor has the wrong size, dtype or device")
-    rc = _lib().mchecksum_gpu_checksum_offsets(method.encode(), data.data_ptr(), offsets.data_ptr(), count,
-                                               out.data_ptr(), _stream_handle(stream))
+    _same_device(data, offsets=offsets, out=out)
+    with _on(data):
+        rc = _lib().mchecksum_gpu_checksum_offsets(method.encode(), data.data_ptr(), offsets.data_ptr(), count,
+                                                   out.data_ptr(), _stream_handle(stream, data.device))
     if rc != 0:
         _err(rc, "mchecksum_gpu_checksum_offsets")
     return out
@@ -140,11 +172,14 @@ def verify_offsets(method: str, data: torch.Tensor, offsets: torch.Tensor, expec
     count = offsets.numel() - 1
     if expected.numel() < count or expected.dtype != out_dtype(method) or not expected.is_cuda:
         raise GpuChecksumError("expected has the wrong size, dtype or device")
-    status = torch.empty(count, dtype=torch.uint8, device=data.device)
+    _same_device(data, offsets=offsets, expected=expected)
+    # status starts "failed": only a hashed payload's verdict overwrites it
+    status = torch.ones(count, dtype=torch.uint8, device=data.device)
     mism = torch.zeros(1, dtype=torch.int32, device=data.device)
-    rc = _lib().mchecksum_gpu_verify_offsets(method.encode(), data.data_ptr(), offsets.data_ptr(), count,
-                                             expected.data_ptr(), status.data_ptr(), mism.data_ptr(),
-                                             _stream_handle(stream))
+    with _on(data):
+        rc = _lib().mchecksum_gpu_verify_offsets(method.encode(), data.data_ptr(), offsets.data_ptr(), count,
+                                                 expected.data_ptr(), status.data_ptr(), mism.data_ptr(),
+                                                 _stream_handle(stream, data.device))
     if rc != 0:
         _err(rc, "mchecksum_gpu_verify_offsets")
     return status, mism
@@ -161,15 +196,17 @@ def verify_messages(data: torch.Tensor, msg_offsets: torch.Tensor, payload_offse
     _check_offsets(data, msg_offsets, offsets_host)
     count = msg_offsets.numel() - 1
     if status is None:
-        status = torch.empty(max(count, 0), dtype=torch.uint8, device=data.device)
+        status = torch.ones(max(count, 0), dtype=torch.uint8, device=data.device)
     elif status.dtype != torch.uint8 or status.numel() < count or not status.is_cuda:
         raise GpuChecksumError("status must be a device uint8 tensor of at least count elements")
     mism = torch.zeros(1, dtype=torch.int32, device=data.device) if mismatches is None else mismatches
     if mism.dtype != torch.int32 or not mism.is_cuda:
         raise GpuChecksumError("mismatches must be a device int32 tensor")
-    rc = _lib().mchecksum_gpu_verify_messages(method.encode(), data.data_ptr(), msg_offsets.data_ptr(), count,
-                                              payload_offset, hash_offset, status.data_ptr(), mism.data_ptr(),
-                                              _stream_handle(stream))
+    _same_device(data, msg_offsets=msg_offsets, status=status, mismatches=mism)
+    with _on(data):
+        rc = _lib().mchecksum_gpu_verify_messages(method.encode(), data.data_ptr(), msg_offsets.data_ptr(), count,
+                                                  payload_offset, hash_offset, status.data_ptr(), mism.data_ptr(),
+                                                  _stream_handle(stream, data.device))
     if rc != 0:
         _err(rc, "mchecksum_gpu_verify_messages")
     return status, mism
@@ -214,10 +251,13 @@ class SegmentBatch:
             out = torch.empty(self.nobj, dtype=out_dtype(method), device=self.device)
         elif out.numel() < self.nobj or out.dtype != out_dtype(method) or not out.is_cuda:
             raise GpuChecksumError("out tensor has the wrong size, dtype or device")
+        if out.device != self.device:
+            raise GpuChecksumError(f"out must be on {self.device}")
         base, n = self.meta.data_ptr(), self.nseg
-        rc = _lib().mchecksum_gpu_checksum_segments(method.encode(), base, base + 8 * n, n, base + 16 * n,
-                                                    self.nobj, self.work.data_ptr(), self.work.numel() * 8,
-                                                    out.data_ptr(), _stream_handle(stream))
+        with torch.cuda.device(self.device):
+            rc = _lib().mchecksum_gpu_checksum_segments(method.encode(), base, base + 8 * n, n, base + 16 * n,
+                                                        self.nobj, self.work.data_ptr(), self.work.numel() * 8,
+                                                        out.data_ptr(), _stream_handle(stream, self.device))
         if rc != 0:
             _err(rc, "mchecksum_gpu_checksum_segments")
         return out
@@ -251,10 +291,13 @@ def verify_core_headers(data: torch.Tensor, msg_offsets: torch.Tensor, kind: str
     _check_device_u8(data, "data")
     _check_offsets(data, msg_offsets, offsets_host)
     count = msg_offsets.numel() - 1
-    status = torch.empty(max(count, 0), dtype=torch.uint8, device=data.device)
+    _same_device(data, msg_offsets=msg_offsets)
+    status = torch.ones(max(count, 0), dtype=torch.uint8, device=data.device)
     mism = torch.zeros(1, dtype=torch.int32, device=data.device)
-    rc = _lib().mchecksum_gpu_verify_core_headers(method.encode(), k, data.data_ptr(), msg_offsets.data_ptr(), count,
-                                                  status.data_ptr(), mism.data_ptr(), _stream_handle(stream))
+    with _on(data):
+        rc = _lib().mchecksum_gpu_verify_core_headers(method.encode(), k, data.data_ptr(), msg_offsets.data_ptr(),
+                                                      count, status.data_ptr(), mism.data_ptr(),
+                                                      _stream_handle(stream, data.device))
     if rc != 0:
         _err(rc, "mchecksum_gpu_verify_core_headers")
     return status, mism
@@ -266,8 +309,9 @@ def fill_splitmix(t: torch.Tensor, seed: int, first_word: int = 0, stream=None) 
     if t.data_ptr() % 16:
         raise GpuChecksumError("tensor must be 16-byte aligned")
     B = load_bench_library()
-    rc = B.mck_bench_fill_splitmix(t.data_ptr(), t.numel() * t.element_size(), seed & (2**64 - 1),
-                                   first_word, _stream_handle(stream))
+    with _on(t):
+        rc = B.mck_bench_fill_splitmix(t.data_ptr(), t.numel() * t.element_size(), seed & (2**64 - 1),
+                                       first_word, _stream_handle(stream, t.device))
     if rc != 0:
         raise GpuChecksumError(f"fill_splitmix failed rc={rc}")
     return t

@@ -1,0 +1,145 @@
+"""Fail-closed work queue (include/mchecksum_gpu.h, "Fail closed").
+
+build/libmchecksum_qfault.so is libmchecksum built with -DMCK_QFAULT_TEST=1:
+in every launch that takes the work queue, workgroup 3 gives up the first unit
+of its second chunk, exactly as a wave whose bounded wait timed out would
+(crc_gpu_device.h, for_each_unit).  Such a launch must never report unhashed
+bytes as good -- the contract hg_get_struct relies on when it turns a failed
+check into HG_CHECKSUM_ERROR (/root/reference/src/mercury.c:565-573):
+
+* checksum calls add 1 to the caller's error word (mchecksum_gpu_set_error_word);
+* verify calls add `count` to the mismatch counter, and every payload's status
+  ends as its true verdict or 1 -- never a stale 0 (status is pre-filled with 0
+  here, so only the kernel can have flagged it).
+
+Reference values come from the product library (itself checked against the
+oracle by the parity suites).
+"""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+QLIB = os.path.join(ROOT, "build", "libmchecksum_qfault.so")
+
+
+@pytest.fixture(scope="module")
+def qlib(gpu):
+    assert os.path.exists(QLIB), "build/libmchecksum_qfault.so missing: run make"
+    L = ctypes.CDLL(QLIB)
+    c = ctypes
+    L.mchecksum_gpu_prepare.argtypes = [c.c_char_p]
+    L.mchecksum_gpu_checksum_offsets.argtypes = [c.c_char_p, c.c_void_p, c.c_void_p, c.c_size_t, c.c_void_p,
+                                                 c.c_void_p]
+    L.mchecksum_gpu_checksum_fixed.argtypes = [c.c_char_p, c.c_void_p, c.c_size_t, c.c_size_t, c.c_size_t,
+                                               c.c_void_p, c.c_void_p]
+    L.mchecksum_gpu_verify_offsets.argtypes = [c.c_char_p, c.c_void_p, c.c_void_p, c.c_size_t, c.c_void_p,
+                                               c.c_void_p, c.c_void_p, c.c_void_p]
+    L.mchecksum_gpu_set_error_word.argtypes = [c.c_void_p]
+    L.mchecksum_gpu_queue_faults.restype = c.c_longlong
+    return L
+
+
+@pytest.fixture(scope="module")
+def batch(gpu):
+    """20000 payloads U[64 B, 8 KiB] packed at byte granularity: > 1024 payloads,
+    so the throughput layout with the work queue runs."""
+    import torch
+    rng = np.random.default_rng(2024)
+    lens = rng.integers(64, 8193, 20000)
+    off = np.zeros(len(lens) + 1, dtype=np.int64)
+    off[1:] = np.cumsum(lens)
+    data = torch.empty(int(off[-1]) + 64, dtype=torch.uint8, device="cuda")
+    gpu.fill_splitmix(data, 0xFA17)
+    return data, torch.from_numpy(off).cuda()
+
+
+@pytest.mark.parametrize("method", ["crc32c", "crc64"])
+def test_checksum_fault_bumps_error_word(gpu, qlib, batch, method):
+    import torch
+    data, offs = batch
+    n = offs.numel() - 1
+    want = gpu.checksum_offsets(method, data, offs)
+    out = ~want  # every entry wrong until a launch writes it
+    word = torch.zeros(1, dtype=torch.int32, device="cuda")
+    faults0 = qlib.mchecksum_gpu_queue_faults()
+    assert qlib.mchecksum_gpu_prepare(method.encode()) == 0
+    qlib.mchecksum_gpu_set_error_word(word.data_ptr())
+    try:
+        rc = qlib.mchecksum_gpu_checksum_offsets(method.encode(), data.data_ptr(), offs.data_ptr(), n,
+                                                 out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    finally:
+        qlib.mchecksum_gpu_set_error_word(None)
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert int(word.item()) == 1, "a launch that dropped a unit must bump the error word"
+    assert qlib.mchecksum_gpu_queue_faults() - faults0 == 1
+    lost = np.nonzero((out != want).cpu().numpy())[0]
+    assert len(lost) == 1, lost[:8]  # exactly the injected unit went unhashed; the rest is right
+
+
+def test_verify_fault_fails_closed(gpu, qlib, batch):
+    import torch
+    data, offs = batch
+    n = offs.numel() - 1
+    truth = gpu.checksum_offsets("crc32c", data, offs)
+    expected = truth.clone()
+    bad = np.arange(0, n, 7)
+    expected[torch.from_numpy(bad).cuda()] ^= 0x100  # a genuine mismatch every 7th payload
+    status = torch.zeros(n, dtype=torch.uint8, device="cuda")  # stale "pass" everywhere
+    mism = torch.zeros(1, dtype=torch.int32, device="cuda")
+    assert qlib.mchecksum_gpu_verify_offsets(b"crc32c", data.data_ptr(), offs.data_ptr(), n, expected.data_ptr(),
+                                             status.data_ptr(), mism.data_ptr(),
+                                             torch.cuda.current_stream().cuda_stream) == 0
+    torch.cuda.synchronize()
+    st = status.cpu().numpy()
+    assert int(mism.item()) >= n, "a faulted verify must not read as clean"
+    assert set(np.unique(st).tolist()) <= {0, 1}
+    assert np.all(st[bad] == 1), "a real mismatch read as verified"
+    # every 0 is a payload whose bytes really match; the unhashed one is among
+    # the 1s (the status sweep left it flagged)
+    ok = st == 0
+    assert np.array_equal(expected.cpu().numpy()[ok], truth.cpu().numpy()[ok])
+    assert int((st == 1).sum()) > len(bad)
+
+
+def test_large_fixed_batch_fault(gpu, qlib):
+    """A >= 512 MiB aligned CRC-32C batch (non-temporal loads) also takes the
+    queue: same report."""
+    import torch
+    count, length = 8192, 65536
+    data = torch.empty(count * length + 64, dtype=torch.uint8, device="cuda")
+    gpu.fill_splitmix(data, 0x5EED)
+    want = gpu.checksum_fixed("crc32c", data, length, count=count)
+    out = ~want
+    word = torch.zeros(1, dtype=torch.int32, device="cuda")
+    qlib.mchecksum_gpu_set_error_word(word.data_ptr())
+    try:
+        assert qlib.mchecksum_gpu_checksum_fixed(b"crc32c", data.data_ptr(), length, length, count, out.data_ptr(),
+                                                 torch.cuda.current_stream().cuda_stream) == 0
+    finally:
+        qlib.mchecksum_gpu_set_error_word(None)
+    torch.cuda.synchronize()
+    assert int(word.item()) == 1
+    assert int((out != want).sum().item()) == 1
+
+
+def test_product_library_reports_no_fault(gpu, batch):
+    """The same calls through the product library: error word stays 0."""
+    import torch
+    data, offs = batch
+    word = torch.zeros(1, dtype=torch.int32, device="cuda")
+    gpu.set_error_word(word)
+    try:
+        for method in ("crc32c", "crc64"):
+            gpu.checksum_offsets(method, data, offs)
+        exp = gpu.checksum_offsets("crc32c", data, offs)
+        st, m = gpu.verify_offsets("crc32c", data, offs, exp)
+    finally:
+        gpu.set_error_word(None)
+    torch.cuda.synchronize()
+    assert int(word.item()) == 0 and int(m.item()) == 0 and int(st.sum().item()) == 0

@@ -190,3 +190,55 @@ def test_graph_slot_is_never_reused_by_eager_launches(gpu, oracle_mod, monkeypat
     _wait(torch, "final", (s, e))
     torch.cuda.synchronize()
     assert bad == 0 and G.queue_faults() == 0
+
+
+def test_captured_launches_sharing_one_slot_stay_correct(gpu, oracle_mod):
+    """Two graphs captured onto ONE work-queue slot (MCHECKSUM_GPU_CAPTURED_SLOTS=1,
+    a test knob read once per process -- so this runs in a child process) and
+    replayed concurrently on two streams: the slot's owner word sends whichever
+    launch finds it taken to the static split, so both keep returning the
+    oracle's values (crc_gpu_device.h, "Ownership")."""
+    import subprocess
+    import sys
+    code = r"""
+import os, sys, numpy as np, torch
+sys.path.insert(0, os.environ["ROOT"])
+from mercury_amd import gpu as G
+from oracle import oracle as O
+host = O.splitmix_bytes(8 << 20, 31337)
+dev = torch.cat([torch.from_numpy(host).cuda(), torch.zeros(64, dtype=torch.uint8, device="cuda")])
+rng = np.random.default_rng(5)
+tabs, wants, outs, graphs = [], [], [], []
+for k in range(2):
+    offs = np.zeros(3001, dtype=np.uint64)
+    offs[1:] = np.cumsum(rng.integers(0, 2600, 3000))
+    tabs.append(torch.from_numpy(offs.astype(np.int64)).cuda())
+    wants.append(O.batch_offsets("crc32c", host, offs, nthreads=8))
+    outs.append(torch.zeros(3000, dtype=torch.int32, device="cuda"))
+G.prepare("crc32c")
+torch.cuda.synchronize()
+streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+for k in range(2):
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(streams[k]), torch.cuda.graph(g, stream=streams[k]):
+        G.checksum_offsets("crc32c", dev, tabs[k], out=outs[k])
+    graphs.append(g)
+torch.cuda.synchronize()
+bad = 0
+for rep in range(200):
+    for k in range(2):
+        outs[k].zero_()
+    torch.cuda.synchronize()
+    for k in range(2):
+        with torch.cuda.stream(streams[k]):
+            graphs[k].replay()
+    torch.cuda.synchronize()
+    for k in range(2):
+        bad += int(not np.array_equal(G.as_unsigned(outs[k]).astype(np.uint64), wants[k]))
+print("bad", bad, "faults", G.queue_faults(), flush=True)
+sys.exit(0 if bad == 0 and G.queue_faults() == 0 else 1)
+"""
+    env = dict(os.environ, MCHECKSUM_GPU_CAPTURED_SLOTS="1", MCHECKSUM_GPU_LIGHT="0",
+               ROOT=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]

@@ -6,7 +6,11 @@ workgroup leaves the slot's counters at zero for the next launch.
 
 Each wave is a generator that yields at every access to shared state (LDS or
 the global slot), so a seeded scheduler explores many orders of the same
-steps the device code takes.  Fetch triggers, chunk sizes (chunk_log2, the
+steps the device code takes.  Slot ownership (a launch claims the slot's owner
+word with its tag -- read first, CAS while it is 0; a workgroup that finds it
+held by another launch takes the static split and never touches the slot; the
+last group releases the owner word last) and the fail-closed fault flag are
+modelled too, including two launches that meet on one slot.  Fetch triggers, chunk sizes (chunk_log2, the
 quarter-size tail chunks of ChunkPlan), the
 round-robin sub-queues, the LDS ring recycling and the hierarchical exit
 counting mirror the device code one to one.
@@ -31,6 +35,12 @@ class Slot:
         self.sub = [0] * QSUB          # sub-queue tickets
         self.group_done = [0] * QSUB   # exited workgroups per group
         self.all_done = 0
+        self.fault = 0                 # first faulting wave of the launch
+        self.owner = 0                 # tag of the launch using the slot
+
+    def clean(self):
+        return (self.sub == [0] * QSUB and self.group_done == [0] * QSUB and self.all_done == 0
+                and self.fault == 0 and self.owner == 0)
 
 
 class Lds:
@@ -40,11 +50,44 @@ class Lds:
         self.exited = 0
         self.reads = [0] * RING
         self.entry = [(0xFFFFFFFF, 0)] * RING
+        self.busy = False
+        self.ready = False  # wg_queue_init done (the kernel's barrier)
 
 
-def run_model(n, grid, waves_per_wg, seed, slot=None, max_steps=2_000_000):
+def run_model(n, grid, waves_per_wg, seed, slot=None, max_steps=2_000_000, tag=1, drop=None):
+    """One launch; returns (sorted processed units, slot)."""
+    res = run_launches([dict(n=n, grid=grid, wpw=waves_per_wg, tag=tag, drop=drop)], seed, slot, max_steps)
+    return res[0]["units"], res[0]["slot"]
+
+
+def run_launches(launches, seed, slot=None, max_steps=4_000_000):
+    """Several launches on ONE slot, their waves interleaved at random.
+    drop=(wg, seq): that workgroup's wave taking slot 0 of chunk `seq` gives up
+    (MCK_QFAULT_TEST)."""
     rnd = random.Random(seed)
     slot = slot or Slot()
+    gens = []
+    results = []
+    for spec in launches:
+        r = dict(units=[], slot=slot, faulted_waves=0, first_faults=0, busy_wgs=0)
+        results.append(r)
+        gens += _launch(spec, slot, rnd, r)
+    steps = 0
+    while gens:
+        g = rnd.choice(gens)
+        try:
+            next(g)
+        except StopIteration:
+            gens.remove(g)
+        steps += 1
+        assert steps < max_steps, "no progress: a wait never ends"
+    for r in results:
+        r["units"].sort()
+    return results
+
+
+def _launch(spec, slot, rnd, res):
+    n, grid, waves_per_wg, tag, drop = spec["n"], spec["grid"], spec["wpw"], spec["tag"], spec.get("drop")
     cl = chunk_log2(n, grid)
     cu, lead = 1 << cl, max(1, (1 << cl) // 4) if (1 << cl) > 4 else 1
     # ChunkPlan: full chunks, then about one full chunk per workgroup of units
@@ -60,7 +103,7 @@ def run_model(n, grid, waves_per_wg, seed, slot=None, max_steps=2_000_000):
 
     def size(cid):
         return 1 << cl if cid < nbig else 1 << sl
-    done_units = []
+    done_units = res["units"]
     lds = [Lds() for _ in range(grid)]
 
     def fetch(L, b):  # wg_fetch
@@ -88,8 +131,19 @@ def run_model(n, grid, waves_per_wg, seed, slot=None, max_steps=2_000_000):
         L.entry[r] = (seq, cid)
         yield
 
-    def wave(b):  # for_each_unit<true>
+    def wave(b, w):  # for_each_unit<true>
         L = lds[b]
+        while not L.ready:  # the kernel's first barrier
+            yield
+        if L.busy:  # the slot belongs to another launch: static split, slot untouched
+            nw = grid * waves_per_wg
+            u = b * waves_per_wg + w
+            while u < n:
+                done_units.append(u)
+                u += nw
+                yield
+            return
+        flt = False
         while True:
             t = L.slot
             L.slot += 1
@@ -103,6 +157,9 @@ def run_model(n, grid, waves_per_wg, seed, slot=None, max_steps=2_000_000):
             if (t & (cu - 1)) == cu - lead:
                 nid = NOCH if e[1] == NOCH else (yield from fetch(L, b))
                 yield from publish(L, seq + 1, nid)
+            if drop is not None and (b, seq) == drop and (t & (cu - 1)) == 0:
+                flt = True  # injected give-up: this unit is never hashed
+                e = (seq, NOCH)
             if e[1] == NOCH:
                 break
             k = t & (cu - 1)
@@ -111,6 +168,12 @@ def run_model(n, grid, waves_per_wg, seed, slot=None, max_steps=2_000_000):
                 done_units.append(u)
                 for _ in range(rnd.randint(0, 40)):
                     yield
+        if flt:
+            res["faulted_waves"] += 1
+            first = slot.fault == 0  # atomicCAS(fault, 0, 1)
+            slot.fault = 1
+            yield
+            res["first_faults"] += first
         # hierarchical exit counting
         prev_ex = L.exited  # atomicAdd on LDS: the returned old value decides
         L.exited += 1
@@ -130,23 +193,27 @@ def run_model(n, grid, waves_per_wg, seed, slot=None, max_steps=2_000_000):
                     slot.sub = [0] * QSUB
                     slot.group_done = [0] * QSUB
                     slot.all_done = 0
+                    slot.fault = 0
+                    yield  # s_waitcnt vmcnt(0): the zeros land before ...
+                    slot.owner = 0  # ... the owner word is released
 
-    # wg_queue_init (thread 0 of every workgroup, before the barrier)
-    for b in range(grid):
-        g = (lambda L=lds[b], b=b: (yield from publish(L, 0, (yield from fetch(L, b)))))()
-        for _ in g:
-            pass
-    gens = [wave(b) for b in range(grid) for _ in range(waves_per_wg)]
-    steps = 0
-    while gens:
-        g = rnd.choice(gens)
-        try:
-            next(g)
-        except StopIteration:
-            gens.remove(g)
-        steps += 1
-        assert steps < max_steps, "no progress: a wait never ends"
-    return sorted(done_units), slot
+    def init(b):  # wg_queue_init (thread 0 of the workgroup, before the barrier)
+        L = lds[b]
+        owner = slot.owner  # atomic load first ...
+        yield
+        if owner == 0:  # ... then atomicCAS(owner, 0, tag)
+            owner = slot.owner
+            if owner == 0:
+                slot.owner = tag
+            yield
+        L.busy = owner not in (0, tag)
+        if L.busy:
+            res["busy_wgs"] += 1
+        else:
+            yield from publish(L, 0, (yield from fetch(L, b)))
+        L.ready = True
+
+    return [init(b) for b in range(grid)] + [wave(b, w) for b in range(grid) for w in range(waves_per_wg)]
 
 
 @pytest.mark.parametrize("n,grid", [(1, 1), (2, 3), (17, 1), (67, 2), (67, 5), (100, 3), (257, 8), (1000, 9),
@@ -154,9 +221,9 @@ def run_model(n, grid, waves_per_wg, seed, slot=None, max_steps=2_000_000):
 def test_every_unit_once_and_slot_reset(n, grid):
     slot = Slot()
     for seed in range(3):
-        units, slot = run_model(n, grid, 4, seed * 7919 + n, slot)  # the slot is reused, as by the next launch
+        units, slot = run_model(n, grid, 4, seed * 7919 + n, slot, tag=seed + 1)  # reused by the next launch
         assert units == list(range(n))
-        assert slot.sub == [0] * QSUB and slot.group_done == [0] * QSUB and slot.all_done == 0
+        assert slot.clean()
 
 
 def test_chunk_size_rule():
@@ -171,4 +238,35 @@ def test_chunk_size_rule():
 def test_sixteen_waves_per_workgroup(n, grid):
     units, slot = run_model(n, grid, 16, n + grid)
     assert units == list(range(n))
-    assert slot.sub == [0] * QSUB and slot.all_done == 0
+    assert slot.clean()
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_two_launches_on_one_slot_hash_everything(seed):
+    """Two launches meet on one slot (different tags): each hashes every unit;
+    the one that owns the slot runs the queue exactly once per unit, the
+    other's workgroups that found it busy take the static split (units may be
+    hashed twice only when one launch has both kinds of workgroups)."""
+    a = dict(n=700, grid=4, wpw=4, tag=0xA)
+    b = dict(n=500, grid=3, wpw=4, tag=0xB)
+    ra, rb = run_launches([a, b], seed * 31 + 7)
+    for spec, r in ((a, ra), (b, rb)):
+        assert set(r["units"]) == set(range(spec["n"]))
+        if r["busy_wgs"] in (0, spec["grid"]):
+            assert r["units"] == list(range(spec["n"]))
+    # the slot is clean again unless a launch had both kinds of workgroups
+    # (its queue side never completes the exit count: documented degradation)
+    mixed = any(0 < r["busy_wgs"] < s["grid"] for s, r in ((a, ra), (b, rb)))
+    assert ra["slot"].clean() or mixed
+
+
+@pytest.mark.parametrize("n,grid,drop", [(2000, 4, (1, 1)), (5000, 8, (3, 1)), (300, 2, (0, 2))])
+def test_injected_give_up_is_reported_once(n, grid, drop):
+    """MCK_QFAULT_TEST: the dropped unit is the only one not hashed, exactly one
+    wave claims the launch's fault flag (it runs fail_closed), and the slot is
+    clean for the next launch."""
+    r = run_launches([dict(n=n, grid=grid, wpw=4, tag=5, drop=drop)], n + grid)[0]
+    assert r["faulted_waves"] == 1 and r["first_faults"] == 1
+    missing = set(range(n)) - set(r["units"])
+    assert len(missing) == 1 and len(r["units"]) == n - 1
+    assert r["slot"].clean()
