@@ -50,17 +50,22 @@ CONFIGS = {
     # BASELINE configs[0]: host CPU, through the drop-in streaming API
     "c1": ("crc32c", 1024, 4096, 0x4D43310000000001, "cpu"),
 }
-STRONG = {"c5"}  # configs whose count is the GLOBAL batch (split over ranks)
+# configs whose count is the GLOBAL batch, split over the ranks (strong
+# scaling); the others give every rank a batch of that size (weak scaling)
+STRONG = {"c5", "c4", "msgs"}
 
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=1,
+                   help="ranks (one per GPU); without torchrun in the environment bench.py starts them itself")
     p.add_argument("--steps", type=int, default=50)
     # 40: the clock settles after ~30 back-to-back launches (per-launch times
     # 0.62 -> 0.75 -> 0.62 ms over the first 30, profiles/r01/launch_series_metric.json)
     p.add_argument("--warmup", type=int, default=40)
-    p.add_argument("--config", default="metric", choices=sorted(CONFIGS))
+    p.add_argument("--config", default=None, choices=sorted(CONFIGS),
+                   help="default: the headline (metric) at 1 GPU, C5's 2^20 x 64 KiB global batch split over "
+                        "the ranks at N > 1")
     p.add_argument("--streams", type=int, default=1,
                    help="issue consecutive steps round-robin on this many streams (independent batches, "
                         "fixed and offsets layouts)")
@@ -72,8 +77,38 @@ def parse():
     return p.parse_args()
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args) -> int:
+    """`bench.py --gpus N` outside torchrun: start the N ranks as a child
+    torch.distributed.run (127.0.0.1 rendezvous) BEFORE this process touches
+    the GPU, and return its exit code.  Ranks then see WORLD_SIZE = N."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only (RCCL, CUDA-tensor sharing)
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args))
+    if env_world is not None and int(env_world) != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world}")
+    if args.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    if args.config is None:
+        args.config = "metric" if args.gpus == 1 else "c5"
     if CONFIGS[args.config][4] == "cpu":
         return bench_c1(args)
     import torch
@@ -93,26 +128,32 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
 
     from mercury_amd import gpu as G
-    from mercury_amd.shard import fixed_shard
+    from mercury_amd.shard import batch_shard
+    from mercury_amd.workload import varlen_offsets
 
     method, count, length, seed, layout = CONFIGS[args.config]
     strong = args.config in STRONG
-    if strong:
-        count = fixed_shard(rank, world, count)[1]  # equal shards of the global batch
+    # ONE global batch, split into contiguous rank shares (mercury_amd.shard):
+    # strong configs split their own count; weak ones grow it with the ranks
+    global_count = count if strong else count * world
+    plan = None
+    if layout == "fixed":
+        plan = batch_shard(rank, world, global_count, length)
+    elif layout in ("offsets", "messages"):
+        plan = batch_shard(rank, world, global_count, offsets_global=varlen_offsets(seed, global_count))
+    if plan is not None:
+        count = plan.count
     stream = torch.cuda.current_stream()
     G.prepare(method)
 
-    # ---- per-rank shard of a global batch, generated on the device -------
+    # ---- this rank's share of the global batch, generated on the device ----
     if layout == "fixed":
-        nbytes = count * length
-        data = torch.empty(nbytes + 64, dtype=torch.uint8, device=dev)
-        first_payload, _ = fixed_shard(rank, world, count * world)  # shard r = payloads [r*count, (r+1)*count)
-        first_word = first_payload * length // 8
-        G.fill_splitmix(data, seed, first_word=first_word)
+        data = torch.empty(plan.nbytes + 64, dtype=torch.uint8, device=dev)
+        G.fill_splitmix(data, seed, first_word=plan.first_word)  # the global stream's bytes
         offsets_dev = offsets_host = None
-        payload_bytes = nbytes
+        payload_bytes = plan.nbytes
         run = lambda out: G.checksum_fixed(method, data, length, count=count, out=out)  # noqa: E731
-    elif layout == "segments":
+    elif layout == "segments":  # per-rank objects (weak): scattered segment lists
         from mercury_amd.workload import segment_slots
         seg_len = length // SEGS_PER_OBJECT
         payload_bytes = count * length
@@ -124,11 +165,10 @@ def main():
         offsets_dev = offsets_host = None
         run = lambda out: batch.checksum(method, out=out)  # noqa: E731
     elif layout == "messages":
-        from mercury_amd.workload import varlen_offsets
-        msg_host = varlen_offsets(seed ^ rank, count)
-        payload_bytes = int(msg_host[-1])
-        data = torch.empty(payload_bytes + 64, dtype=torch.uint8, device=dev)
-        G.fill_splitmix(data, seed ^ rank)
+        msg_host = plan.offsets
+        payload_bytes = int(msg_host[-1] - msg_host[0])
+        data = torch.empty(plan.nbytes + 64, dtype=torch.uint8, device=dev)
+        G.fill_splitmix(data, seed, first_word=plan.first_word)
         # sender side (hg_set_struct): CRC of each payload = message bytes
         # [20, len); one offsets batch over the interleaved table
         # (header_i, payload_i, ...), the checker's layout as well
@@ -148,11 +188,10 @@ def main():
         G.verify_messages(data, msg_dev, status=status, mismatches=mism, offsets_host=msg_host)  # validates once
         run = lambda out: G.verify_messages(data, msg_dev, status=status, mismatches=mism)  # noqa: E731
     else:
-        from mercury_amd.workload import varlen_offsets
-        offsets_host = varlen_offsets(seed ^ rank, count)
-        payload_bytes = int(offsets_host[-1])
-        data = torch.empty(payload_bytes + 64, dtype=torch.uint8, device=dev)
-        G.fill_splitmix(data, seed ^ rank)
+        offsets_host = plan.offsets
+        payload_bytes = int(offsets_host[-1] - offsets_host[0])
+        data = torch.empty(plan.nbytes + 64, dtype=torch.uint8, device=dev)
+        G.fill_splitmix(data, seed, first_word=plan.first_word)
         offsets_dev = torch.from_numpy(offsets_host.astype(np.int64)).to(dev)
         G.checksum_offsets(method, data, offsets_dev, offsets_host=offsets_host)  # validates the table once
         run = lambda out: G.checksum_offsets(method, data, offsets_dev, out=out)  # noqa: E731
@@ -191,9 +230,12 @@ def main():
 
     coll_dev = dev if args.backend == "nccl" else torch.device("cpu")
     t = torch.tensor([wall, kern_ms], dtype=torch.float64, device=coll_dev)
+    per_rank = [t.clone() for _ in range(world)]
     if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    wall_max, kern_ms_max = float(t[0]), float(t[1])
+        dist.all_gather(per_rank, t)
+    per_rank = [[float(x[0]), float(x[1])] for x in per_rank]
+    wall_max = max(w for w, _ in per_rank)
+    kern_ms_max = max(k for _, k in per_rank)
 
     # ---- gathered result (outside the timed region) ----------------------
     crcs = out
@@ -211,14 +253,21 @@ def main():
         verify_note = (f"{args.steps + args.warmup + 1} verify launches: {bad_before} mismatches; one flipped bit "
                        f"flagged {flagged} (expected [{victim}])")
         crcs = sender  # the sender-side CRCs, checked against the oracle below
-    if world > 1:
-        mine = out.to(coll_dev)
+    if world > 1 and layout != "messages":
+        # RCCL all_gather of the per-rank CRC arrays (padded to the largest
+        # shard: ranks may hold different counts), then trimmed in rank order
+        counts = plan.counts if plan is not None else [count] * world
+        mine = torch.zeros(max(counts), dtype=crcs.dtype, device=coll_dev)
+        mine[:count] = crcs[:count].to(coll_dev)
         gathered = [torch.empty_like(mine) for _ in range(world)]
         dist.all_gather(gathered, mine)
-        crcs = torch.cat(gathered)
+        crcs = torch.cat([g[:c] for g, c in zip(gathered, counts)])
     got = G.as_unsigned(crcs) if rank == 0 else None
 
-    total_bytes = payload_bytes * world * args.steps  # every rank checksummed its shard once per step
+    bytes_all = torch.tensor([float(payload_bytes)], dtype=torch.float64, device=coll_dev)
+    if world > 1:
+        dist.all_reduce(bytes_all)
+    total_bytes = float(bytes_all[0]) * args.steps  # every rank checksummed its shard once per step
     gib_s = total_bytes / wall_max / 2**30
     out_bytes = count * (4 if G.out_dtype(method) == torch.int32 else 8)
     alg_bytes = payload_bytes + out_bytes + (8 * (count + 1) if layout == "offsets" else 0) + \
@@ -229,16 +278,22 @@ def main():
 
     result = None
     if rank == 0:
-        traffic = None
+        # HBM bytes per launch cannot be counted inside this process: they come
+        # from the committed rocprofv3 PMC passes of this same command
+        # (tools/gpu_pmc_traffic.sh -> profiles/pmc_traffic_<config>.json)
+        traffic, traffic_src = None, None
         pmc = os.path.join(ROOT, "profiles", f"pmc_traffic_{args.config}.json")
-        if os.path.exists(pmc):
+        if os.path.exists(pmc) and world == 1:
             try:
                 traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+                traffic_src = (f"profiles/pmc_traffic_{args.config}.json (rocprofv3 FETCH_SIZE + WRITE_SIZE passes "
+                               "of this config, committed; not measured in this run)")
             except Exception:
                 traffic = None
+        metric = {"metric": "GiB/s checksummed (device-resident), CRC32c, 64K x 64 KiB payloads",
+                  "c5": "GiB/s checksummed (device-resident), CRC32c, 1M x 64 KiB payloads split over the GPUs (C5)"}
         result = {
-            "metric": "GiB/s checksummed (device-resident), CRC32c, 64K x 64 KiB payloads"
-            if args.config == "metric" else f"GiB/s checksummed (device-resident), {args.config}",
+            "metric": metric.get(args.config, f"GiB/s checksummed (device-resident), {args.config}"),
             "value": round(gib_s, 2),
             "unit": "GiB/s",
             "n_gpus": world,
@@ -250,15 +305,22 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (splitmix64 bytes generated on device)",
-            "config": {"workload": f"{method} over {count} x {length if length else 'U[64B,64KiB]'} B payloads per GPU"
+            "config": {"workload": f"{args.config}: {method} over {global_count} x "
+                       f"{length if length else 'U[64B,64KiB]'} B payloads"
                        + (" (offsets table)" if layout == "offsets" else "")
                        + (" as Mercury messages, verified in place" if layout == "messages" else "")
-                       + (f" ({SEGS_PER_OBJECT} scattered segments each)" if layout == "segments" else ""),
-                       "method": method, "payloads_per_gpu": count, "payload_bytes": length,
-                       "bytes_per_gpu": payload_bytes, "lanes_per_payload": G.lanes_per_payload(method, length or 65536)
-                       if layout == "fixed" else 64, "parallelism": f"shard{world}"},
+                       + (f" ({SEGS_PER_OBJECT} scattered segments each)" if layout == "segments" else "")
+                       + (f", one global batch split over {world} GPUs" if world > 1 and layout != "segments"
+                          else f", per GPU" if world > 1 else ""),
+                       "method": method, "global_batch": global_count, "payloads_rank0": count,
+                       "payload_bytes": length, "bytes_rank0": payload_bytes,
+                       "lanes_per_payload": G.lanes_per_payload(method, length or 65536) if layout == "fixed" else 64,
+                       "parallelism": f"shard{world}"},
+            "world_size": dist.get_world_size() if world > 1 else 1,
+            "per_rank": [{"rank": r, "wall_ms_per_step": round(w / args.steps * 1e3, 4), "kernel_ms": round(k, 4)}
+                         for r, (w, k) in enumerate(per_rank)],
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
                          "kernel_ms": round(kern_ms_max, 4), "algorithmic_bytes_per_launch": alg_bytes},
         }
         if world == 1 and not args.no_cpu_baseline:
@@ -270,8 +332,8 @@ def main():
         elif world > 1 and layout == "messages":
             result["parity"] = "per-rank verify counters (see verify)"
         elif world > 1:
-            result["parity"] = cross_rank_check(G, method, seed, length, offsets_host, got, count, world, dev,
-                                                args.parity_samples, segments=layout == "segments")
+            result["parity"] = cross_rank_check(G, method, seed, length, got, world, dev, args.parity_samples,
+                                                layout, global_count, count)
         else:
             result["parity"] = "unchecked (--no-cpu-baseline)"
         if verify_note:
@@ -333,6 +395,17 @@ def _segment_object_bytes(O, seed, length, j, slots):
                            for q in range(SEGS_PER_OBJECT)])
 
 
+def _cpu_quota():
+    """The cgroup v2 CPU limit as (CPUs,), e.g. cpu.max "1600000 100000" -> (16.0,); None if unlimited."""
+    try:
+        q = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q and q[0] != "max":
+            return (int(q[0]) / int(q[1]),)
+    except (OSError, ValueError, IndexError, ZeroDivisionError):
+        pass
+    return None
+
+
 def _cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -350,7 +423,13 @@ def cpu_baseline(method, seed, length, offsets_host, got, budget_s, samples, seg
     payloads), whose CRCs then check the GPU's values for those payloads; plus
     `samples` random payloads from the whole batch."""
     from oracle import oracle as O
-    threads = max(1, min(16, os.cpu_count() or 1))
+    # `nproc` threads (BASELINE.md "Thread counts"): every CPU this process may
+    # run on -- capped by the cgroup CPU quota when the box sets one (the GPU
+    # box grants 16 CPUs of a 128-thread host: 256 threads on that quota ran
+    # 4x slower than 16)
+    affinity = len(os.sched_getaffinity(0))
+    quota = _cpu_quota()
+    threads = max(1, min(256, affinity, int(quota[0]) if quota else affinity))
     variant = "sse42" if method == "crc32c" else "table"
     slots = None
     if segments:
@@ -375,17 +454,24 @@ def cpu_baseline(method, seed, length, offsets_host, got, budget_s, samples, seg
         sample_bytes = int(offsets_host[n])
         what = f"the first {n} payloads ({sample_bytes} B) of the offsets layout"
     run = lambda k: runv(k, variant, threads)  # noqa: E731
-    run(64)  # warm
-    passes, t0 = 0, time.perf_counter()
+    for _ in range(3):  # warm-ups
+        run(n)
+    # per-pass CLOCK_MONOTONIC times (time.perf_counter), >= 20 passes or the
+    # wall budget; the value is the median pass
+    laps, t0 = [], time.perf_counter()
     while True:
+        ta = time.perf_counter()
         want = run(n)
-        passes += 1
+        laps.append(time.perf_counter() - ta)
         el = time.perf_counter() - t0
-        if el >= budget_s and passes >= 2:
+        if (el >= budget_s and len(laps) >= 5) or (len(laps) >= 20 and el >= budget_s / 4) or len(laps) >= 2000:
             break
-    base = {"value": round(passes * sample_bytes / el / 2**30, 2), "unit": "GiB/s", "cores": threads, "kind": "port",
+    med = float(np.median(laps))
+    base = {"value": round(sample_bytes / med / 2**30, 2), "unit": "GiB/s", "cores": threads, "kind": "port",
             "variant": "x86 SSE4.2 crc32 instruction" if variant == "sse42" else "slicing table",
-            "sample": f"{passes} passes over {what} of the same splitmix payloads ({el:.2f} s wall)"}
+            "sample": f"median of {len(laps)} passes over {what} of the same splitmix payloads "
+                      f"({el:.2f} s wall, {threads} threads)"}
+    base["cpus_visible"] = f"{affinity} in the affinity mask" + (f", cgroup quota {quota[0]:g} CPUs" if quota else "")
     # the other CPU paths on the same sample: 1 thread, and the
     # table path next to SSE4.2 for CRC-32C
     legs = [("sse42" if variant == "sse42" else "table", 1)] + ([("table", threads)] if variant == "sse42" else [])
@@ -423,46 +509,49 @@ def cpu_baseline(method, seed, length, offsets_host, got, budget_s, samples, seg
     return base, parity
 
 
-def cross_rank_check(G, method, seed, length, offsets_host, got, count, world, dev, samples, segments=False):
-    """N>1 (rank 0): regenerate sampled payloads of EVERY shard on rank 0's GPU
-    and recompute them through the same entry point; the gathered CRCs must
-    agree (kernel parity itself is the N=1 oracle check and tests/)."""
+def cross_rank_check(G, method, seed, length, got, world, dev, samples, layout, global_count, count0):
+    """N>1 (rank 0): regenerate sampled payloads of EVERY rank's share on rank
+    0's GPU and recompute them through the same entry point; the gathered CRCs
+    (global payload order) must agree.  Kernel parity itself is the N=1 oracle
+    check and tests/."""
     if got is None:
         return None
     import torch
     from mercury_amd.workload import varlen_offsets
     rng = np.random.default_rng(4321)
     bad = checked = 0
-    for r in range(world):
-        idx = np.unique(np.concatenate([[0, count - 1], rng.integers(0, count, max(1, samples // world))]))
-        off_r = None if offsets_host is None else varlen_offsets(seed ^ r, count)
-        if segments:
-            from mercury_amd.workload import segment_slots
-            slots = segment_slots(seed ^ r, count * SEGS_PER_OBJECT)
-        for i in idx:
-            i = int(i)
-            if segments:
-                seg = length // SEGS_PER_OBJECT
+    if layout == "segments":  # weak: rank r's objects from seed ^ r, count0 per rank
+        from mercury_amd.workload import segment_slots
+        seg = length // SEGS_PER_OBJECT
+        for r in range(world):
+            slots = segment_slots(seed ^ r, count0 * SEGS_PER_OBJECT)
+            for i in np.unique(np.concatenate([[0, count0 - 1], rng.integers(0, count0, max(1, samples // world))])):
                 parts = []
                 for q in range(SEGS_PER_OBJECT):
                     t = torch.empty(seg + 64, dtype=torch.uint8, device=dev)
-                    G.fill_splitmix(t, seed ^ r, first_word=int(slots[i * SEGS_PER_OBJECT + q]) * seg // 8)
+                    G.fill_splitmix(t, seed ^ r, first_word=int(slots[int(i) * SEGS_PER_OBJECT + q]) * seg // 8)
                     parts.append(t[:seg])
-                v = G.checksum_segments(method, parts)
-            elif off_r is None:
+                bad += int(G.as_unsigned(G.checksum_segments(method, parts))[0] != got[r * count0 + int(i)])
+                checked += 1
+    else:
+        off = varlen_offsets(seed, global_count) if layout == "offsets" else None
+        idx = np.unique(np.concatenate([[0, global_count - 1], rng.integers(0, global_count, samples)]))
+        for i in idx:
+            i = int(i)
+            if off is None:
                 buf = torch.empty(length + 64, dtype=torch.uint8, device=dev)
-                G.fill_splitmix(buf, seed, first_word=(r * count + i) * length // 8)
+                G.fill_splitmix(buf, seed, first_word=i * length // 8)
                 v = G.checksum_fixed(method, buf, length, count=1)
             else:
-                lo, hi = int(off_r[i]), int(off_r[i + 1])
+                lo, hi = int(off[i]), int(off[i + 1])
                 w0 = lo // 8
                 buf = torch.empty(hi - w0 * 8 + 64, dtype=torch.uint8, device=dev)
-                G.fill_splitmix(buf, seed ^ r, first_word=w0)
+                G.fill_splitmix(buf, seed, first_word=w0)
                 t = torch.tensor([lo - w0 * 8, hi - w0 * 8], dtype=torch.int64, device=dev)
                 v = G.checksum_offsets(method, buf, t)
-            bad += int(G.as_unsigned(v)[0] != got[r * count + i])
+            bad += int(G.as_unsigned(v)[0] != got[i])
             checked += 1
-    return (f"consistent ({checked} payloads across {world} shards recomputed on rank 0)" if bad == 0
+    return (f"consistent ({checked} payloads across all {world} shares recomputed on rank 0)" if bad == 0
             else f"MISMATCH {bad}/{checked} across shards")
 
 

@@ -14,7 +14,9 @@ Pins, in order of strength:
                   8(c)) with CRCs per method; CRC-32C cross-checked by SSE4.2,
                   CRC-64/CRC-16 marked parity-unpinned (upstream variant
                   unknown);
-  stream_split.json  update(a); update(b) == update(a||b) split points.
+  stream_split.json  update(a); update(b) == update(a||b) split points;
+  core_headers.json  Mercury core-header request/response images with their
+                  CRC-16 for every catalogue variant (core_header_fixtures).
 The reference's own tests hold no CRC values, so nothing
 here comes from the reference; the data are generated from seeds.
 """
@@ -65,6 +67,51 @@ def test_proc_images():
     return {"uint_struct": (uint_struct, [1, 2, 4, 8]), "string_hello": (string_obj, [8, 6, 1, 1])}
 
 
+CRC16_VARIANTS = [k for k in CATALOGUE if k.startswith("crc16-")]
+
+
+def core_header_fixtures():
+    """Mercury core headers as hg_core_header_request_proc / _response_proc
+    encode them (src/mercury_core_header.c:175-289): the CRC16 runs over the
+    HOST-order field values in proc order (HG_CORE_HEADER_CHECKSUM_UPDATE,
+    :48-55) -- request hg u8, protocol u8, id u64, flags u8, cookie u8 (12 B);
+    response ret_code i8, flags u8, cookie u16 (4 B) -- and the wire carries
+    the fields big-endian (:26-36) with the u16 hash big-endian right after the
+    last field (request offset 12, response offset 4: the response's u64 pad
+    is never proc'd), in a 16-byte header (src/mercury_core_header.h:23-40).
+    One hash per CRC-16 catalogue variant (which one upstream mchecksum's
+    "crc16" is stays unpinned)."""
+    rng_vals = []
+    x = 0x4D43484452000001
+    for i in range(16):  # seeded field values, edges first
+        x = O.splitmix64(x)
+        rng_vals.append(x)
+    reqs = [(0x48 | 0x47, 5, 0, 0, 0), (0xFF, 0xFF, 2**64 - 1, 0xFF, 0xFF), (0x4F, 5, 0x0123456789ABCDEF, 0x81, 0x22)]
+    reqs += [(v & 0xFF, (v >> 8) & 0xFF, O.splitmix64(v), (v >> 16) & 0xFF, (v >> 24) & 0xFF) for v in rng_vals[:8]]
+    resps = [(0, 0, 0), (-1, 0xFF, 0xFFFF), (-128, 0x01, 0x1234), (127, 0x80, 0x8000)]
+    resps += [(((v & 0xFF) ^ 0x80) - 0x80, (v >> 8) & 0xFF, (v >> 16) & 0xFFFF) for v in rng_vals[8:]]
+    out = {"source": "src/mercury_core_header.c:175-289 encodings; CRC16 of the host-order field image per "
+                     "CRC-16 catalogue variant (oracle bitwise model); upstream crc16 variant: parity unpinned",
+           "request": [], "response": []}
+    for hg, proto, rid, flags, cookie in reqs:
+        img = struct.pack("<BBQBB", hg, proto, rid, flags, cookie)
+        e = {"fields": [hg, proto, hex(rid), flags, cookie], "image": img.hex(), "hash_offset": 12,
+             "wire_fields": struct.pack(">BBQBB", hg, proto, rid, flags, cookie).hex()}
+        for v in CRC16_VARIANTS:
+            e[v] = hex(O.crc(v, img, variant="bitwise"))
+            assert int(e[v], 16) == O.crc(v, img)
+        out["request"].append(e)
+    for ret, flags, cookie in resps:
+        img = struct.pack("<bBH", ret, flags, cookie)
+        e = {"fields": [ret, flags, cookie], "image": img.hex(), "hash_offset": 4,
+             "wire_fields": struct.pack(">bBH", ret, flags, cookie).hex()}
+        for v in CRC16_VARIANTS:
+            e[v] = hex(O.crc(v, img, variant="bitwise"))
+            assert int(e[v], 16) == O.crc(v, img)
+        out["response"].append(e)
+    return out
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     cat = {k: {"width": w, "poly": hex(p), "refin": ri, "refout": ro, "init": hex(i), "xorout": hex(x),
@@ -101,6 +148,8 @@ def main():
     json.dump({"source": "payload = splitmix_bytes(offset+length, seed)[offset:]; oracle CRCs; "
                          "crc32c cross-checked with SSE4.2 at generation",
                "vectors": vecs}, open(os.path.join(OUT, "vectors.json"), "w"), indent=1)
+
+    json.dump(core_header_fixtures(), open(os.path.join(OUT, "core_headers.json"), "w"), indent=1)
 
     splits = []
     buf = O.splitmix_bytes(5000, 77)

@@ -1,0 +1,131 @@
+"""bench.py's multi-GPU plumbing on the CPU: the rank launcher, the shard plan
+of one global batch (mercury_amd.shard.batch_shard) and the padded all_gather
+of unequal shards, rehearsed with 2 gloo ranks through the drop-in library's
+streaming API (standing in for the GPU kernels on a CPU-only box)."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_fixed_plan_covers_the_global_batch():
+    from mercury_amd.shard import batch_shard
+    for total in (1, 7, 64, 1 << 20):
+        for world in (1, 2, 3, 5, 8):
+            plans = [batch_shard(r, world, total, 65536) for r in range(world)]
+            assert sum(p.count for p in plans) == total
+            assert [p.first for p in plans] == plans[0].firsts
+            for p in plans:
+                assert p.byte_base == p.first * 65536 and p.nbytes == p.count * 65536
+                assert p.first_word * 8 == p.byte_base and p.counts == plans[0].counts
+
+
+def test_offsets_plan_reproduces_global_bytes(oracle_mod):
+    """Each rank's buffer, generated from its first_word, holds exactly the
+    global batch's bytes of its payloads, and the CRCs of its local payloads
+    are the global ones (C4's generator, 3 ranks)."""
+    from mercury_amd.shard import batch_shard
+    from mercury_amd.workload import varlen_offsets
+    O = oracle_mod
+    seed, total, world = 0x4D43310000000004, 600, 3
+    off = varlen_offsets(seed, total)
+    glob = O.splitmix_bytes(int(off[-1]), seed)
+    want = O.batch_offsets("crc32c", glob, off)
+    got = []
+    plans = [batch_shard(r, world, total, offsets_global=off) for r in range(world)]
+    assert sum(p.count for p in plans) == total
+    sizes = [int(p.offsets[-1] - p.offsets[0]) for p in plans]
+    assert max(sizes) - min(sizes) <= 2 * 65536  # each cut within one payload of its ideal
+    for p in plans:
+        local = O.splitmix_bytes(p.nbytes, seed, first_word=p.first_word)
+        assert np.array_equal(local[int(p.offsets[0]):], glob[p.byte_base + int(p.offsets[0]):p.byte_base + p.nbytes])
+        got.append(O.batch_offsets("crc32c", local, p.offsets))
+    assert np.array_equal(np.concatenate(got), want)
+
+
+def test_world_size_mismatch_is_refused():
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
+
+
+def test_launcher_starts_torchrun_before_touching_the_gpu(monkeypatch):
+    """--gpus N without torchrun: bench.py starts N ranks itself (127.0.0.1
+    rendezvous) and returns their exit code."""
+    sys.path.insert(0, ROOT)
+    import bench
+    seen = {}
+
+    def fake_call(cmd, env):
+        seen["cmd"], seen["env"] = cmd, env
+        return 7
+
+    monkeypatch.setattr(subprocess, "call", fake_call)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "4", "--steps", "3"])
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    with pytest.raises(SystemExit) as e:
+        bench.main()
+    assert e.value.code == 7
+    cmd = seen["cmd"]
+    assert cmd[1:3] == ["-m", "torch.distributed.run"] and "--nproc-per-node=4" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[-4:] == ["--gpus", "4", "--steps", "3"] and cmd[-5].endswith("bench.py")
+    assert seen["env"]["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, total, seed, q):
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+    from mercury_amd import checksum
+    from mercury_amd.shard import batch_shard
+    from mercury_amd.workload import varlen_offsets
+    from oracle import oracle as O
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    off = varlen_offsets(seed, total)
+    p = batch_shard(rank, world, total, offsets_global=off)
+    local = O.splitmix_bytes(p.nbytes, seed, first_word=p.first_word)
+    mine = torch.tensor([checksum("crc32c", local[int(p.offsets[i]):int(p.offsets[i + 1])].tobytes())
+                         for i in range(p.count)], dtype=torch.int64)
+    # bench.py: pad to the largest shard, all_gather, trim in rank order
+    pad = torch.zeros(max(p.counts), dtype=torch.int64)
+    pad[:p.count] = mine
+    gathered = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(gathered, pad)
+    full = torch.cat([g[:c] for g, c in zip(gathered, p.counts)])
+    if rank == 0:
+        want = O.batch_offsets("crc32c", O.splitmix_bytes(int(off[-1]), seed), off)
+        q.put((bool(np.array_equal(full.numpy().astype(np.uint64), want)), len(set(p.counts))))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_global_offsets_batch_split_and_gather():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, 501, 0x4D43310000000004, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    ok, distinct_counts = q.get()
+    assert ok
+    assert distinct_counts == 2  # byte-balanced shares of a random batch: unequal counts, padded gather

@@ -6,8 +6,9 @@
   API fed one update per segment.
 * verify_core_headers: Mercury core headers encoded as
   hg_core_header_request_proc / _response_proc do it
-  (src/mercury_core_header.c:175-289), hashed with the streaming API over the
-  host-order field values, then corrupted in known places.
+  (src/mercury_core_header.c:175-289), hashed by the ORACLE over the
+  host-order field values for every CRC-16 catalogue variant (and the
+  committed request/response fixtures), then corrupted in known places.
 """
 import struct
 
@@ -116,43 +117,58 @@ def test_segments_reject_bad_arguments(gpu, buf):
 
 
 # ------------------------------------------------------------ core headers --
+#
+# The expected hashes come straight from the oracle (oracle.crc over the
+# host-order field image each proc function streams into mchecksum_update,
+# src/mercury_core_header.c:193-205 / 255-261), for every CRC-16 catalogue
+# variant, plus the committed request/response fixtures
+# (tests/golden/core_headers.json, oracle/gen_golden.py).
 
-def _request(rng, ck):
+CRC16_VARIANTS = ["crc16-arc", "crc16-ibm-3740", "crc16-xmodem", "crc16-kermit", "crc16-umts", "crc16-t10-dif"]
+
+
+def _request(rng, oracle_mod, variant):
     hg, proto, rid, flags, cookie = 0x48 | 0x47, 5, int(rng.integers(0, 2**63)), int(rng.integers(0, 256)), \
         int(rng.integers(0, 256))
-    ck.reset()
-    for f in (struct.pack("<B", hg), struct.pack("<B", proto), struct.pack("<Q", rid), struct.pack("<B", flags),
-              struct.pack("<B", cookie)):
-        ck.update(f)  # HG_CORE_HEADER_CHECKSUM_UPDATE: host-order values
-    h = ck.get()
+    img = struct.pack("<BBQBB", hg, proto, rid, flags, cookie)  # HG_CORE_HEADER_CHECKSUM_UPDATE: host order
+    h = oracle_mod.crc(variant, img)
     wire = struct.pack(">BBQBBH", hg, proto, rid, flags, cookie, h) + b"\0\0"  # hash union is 4 bytes
     assert len(wire) == 16
     return wire
 
 
-def _response(rng, ck):
+def _response(rng, oracle_mod, variant):
     ret, flags, cookie = int(rng.integers(-128, 128)), int(rng.integers(0, 256)), int(rng.integers(0, 65536))
-    ck.reset()
-    for f in (struct.pack("<b", ret), struct.pack("<B", flags), struct.pack("<H", cookie)):
-        ck.update(f)
-    h = ck.get()
+    img = struct.pack("<bBH", ret, flags, cookie)
+    h = oracle_mod.crc(variant, img)
     wire = struct.pack(">bBHH", ret, flags, cookie, h) + b"\0" * 10  # pad is never proc'd: hash lands at 4
     assert len(wire) == 16
     return wire
 
 
-@pytest.mark.parametrize("variant", [None, "crc16-arc", "crc16-ibm-3740"])
+def _golden_headers(kind, variant):
+    import json
+    import os
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "core_headers.json")))
+    out = []
+    for e in g[kind]:
+        wire = bytes.fromhex(e["wire_fields"]) + struct.pack(">H", int(e[variant], 16))
+        out.append(wire + b"\0" * (16 - len(wire)))
+    return out
+
+
+@pytest.mark.parametrize("variant", [None] + CRC16_VARIANTS)
 @pytest.mark.parametrize("kind", ["request", "response"])
-def test_core_headers(gpu, kind, variant, monkeypatch):
+def test_core_headers(gpu, oracle_mod, kind, variant, monkeypatch):
     import torch
-    from mercury_amd import Checksum
     if variant:
         monkeypatch.setenv("MCHECKSUM_CRC16_VARIANT", variant)
+    name = variant or "crc16-t10-dif"  # the library's default "crc16"
     rng = np.random.default_rng(31 if kind == "request" else 32)
-    ck = Checksum("crc16")
-    msgs = []
-    for i in range(3000):
-        hdr = (_request if kind == "request" else _response)(rng, ck)
+    gold = _golden_headers(kind, name)
+    msgs = [bytearray(h) for h in gold]
+    for i in range(3000 - len(gold)):
+        hdr = (_request if kind == "request" else _response)(rng, oracle_mod, name)
         body = rng.integers(0, 256, size=int(rng.integers(0, 300)), dtype=np.uint8).tobytes()
         msgs.append(bytearray(hdr + body))
     hash_at = 12 if kind == "request" else 4
@@ -173,12 +189,14 @@ def test_core_headers(gpu, kind, variant, monkeypatch):
 
 
 def test_core_header_values_pinned_to_oracle(oracle_mod):
-    """The encoder above hashes host-order images; pin one against the oracle
-    (default crc16 = CRC-16/T10-DIF, parity unpinned vs upstream mchecksum)."""
+    """The product's streaming CRC16 (fed field by field, as the proc code
+    does) equals the oracle's on a request image (default crc16 =
+    CRC-16/T10-DIF, parity unpinned vs upstream mchecksum)."""
     from mercury_amd import Checksum
     img = struct.pack("<BBQBB", 0x4F, 5, 0x0123456789ABCDEF, 0x81, 0x22)
     ck = Checksum("crc16")
-    ck.update(img)
+    for a, b in ((0, 1), (1, 2), (2, 10), (10, 11), (11, 12)):
+        ck.update(img[a:b])
     assert ck.get() == oracle_mod.crc("crc16", np.frombuffer(img, dtype=np.uint8))
 
 
