@@ -13,7 +13,8 @@
  * whole-buffer form is exact because, in Mercury's default non-XDR build, the
  * proc checksum is the CRC of the contiguous serialized bytes
  * buf[0 : hg_proc_get_size_used) (src/mercury_proc.h:124-143,162-181;
- * SURVEY.md 0.4).
+ * SURVEY.md 0.4).  It is NOT exact for a Mercury built with XDR encoding:
+ * hash such buffers with mchecksum_gpu_checksum_xdr() below.
  *
  * Memory: dev_base, dev_offsets and dev_out are device pointers (hipMalloc or
  * any device-accessible allocation).  Payload bytes are read in aligned
@@ -151,6 +152,52 @@ MCHECKSUM_PUBLIC int
 mchecksum_gpu_verify_core_headers(const char *hash_method, int kind,
     const void *dev_buf, const uint64_t *dev_msg_offsets, size_t count,
     uint8_t *dev_status, uint32_t *dev_mismatches, void *stream);
+
+/* XDR-mode proc checksum.  In a Mercury built with
+ * MERCURY_USE_XDR (HG_HAS_XDR) the serialized buffer holds XDR -- every
+ * integer big-endian and rounded up to 4 bytes, byte arrays zero-padded to a
+ * multiple of 4 -- while the proc checksum covers the HOST-order field values
+ * (src/mercury_proc.h:110-122,147-160).  The whole-buffer entry points above
+ * are exact only for the default non-XDR encoding; they cannot tell an XDR
+ * buffer apart and must not be used on one.  This entry point takes the
+ * message's field schema instead, the sequence of hg_proc_* calls its proc
+ * function makes:
+ *   MCHECKSUM_XDR_INT         size 1, 2, 4 or 8: hg_proc_[u]int<8*size>_t
+ *                             (wire: 4 or 8 bytes big-endian; hashed: the
+ *                             size little-endian bytes of the value)
+ *   MCHECKSUM_XDR_OPAQUE      size bytes of hg_proc_bytes/raw/memcpy (wire:
+ *                             the bytes + zero pad to a multiple of 4)
+ *   MCHECKSUM_XDR_OPAQUE_LEN  as OPAQUE, byte count = the value of the last
+ *                             INT field (hg_string_t: u64 length, then bytes)
+ *   MCHECKSUM_XDR_RAW         size bytes reserved by hg_proc_save_ptr and
+ *                             hashed by hg_proc_restore_ptr (exact size, no
+ *                             XDR rounding; src/mercury_proc.c:277-335)
+ *   MCHECKSUM_XDR_RAW_LEN     as RAW, size = the last INT field's value
+ *                             (bulk handles, src/mercury_proc_bulk.c:91-125)
+ *   MCHECKSUM_XDR_SKIP_IF_ZERO if the last INT field was 0, skip the next
+ *                             `size` schema entries (an empty hg_string_t
+ *                             carries no bytes and no flags)
+ * Message i = dev_buf[dev_msg_offsets[i], dev_msg_offsets[i+1]) starting
+ * where the proc buffer starts; dev_out[i] = the value hg_proc_checksum_get
+ * returns for it (host-order, method size).  dev_status[i] (optional) = 1
+ * when the schema runs past the message (dev_out[i] is then 0).  At most 64
+ * schema entries; reflected 32/64-bit methods (crc32c, crc64). */
+#define MCHECKSUM_XDR_INT          0
+#define MCHECKSUM_XDR_OPAQUE       1
+#define MCHECKSUM_XDR_OPAQUE_LEN   2
+#define MCHECKSUM_XDR_RAW          3
+#define MCHECKSUM_XDR_RAW_LEN      4
+#define MCHECKSUM_XDR_SKIP_IF_ZERO 5
+typedef struct mchecksum_xdr_field {
+    uint32_t kind;
+    uint32_t size;
+} mchecksum_xdr_field_t;
+
+MCHECKSUM_PUBLIC int
+mchecksum_gpu_checksum_xdr(const char *hash_method,
+    const mchecksum_xdr_field_t *fields, size_t nfields, const void *dev_buf,
+    const uint64_t *dev_msg_offsets, size_t count, void *dev_out,
+    uint8_t *dev_status, void *stream);
 
 /* Lanes cooperating on one payload that checksum_fixed would choose for
  * this length (1..64), for reporting; -1 on error. */

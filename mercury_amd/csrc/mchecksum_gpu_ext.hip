@@ -12,12 +12,17 @@
 //    headers (hg_core_header_request_proc / _response_proc,
 //    src/mercury_core_header.c:175-289) for a batch of received messages that
 //    already sit in device memory.
+//  * mchecksum_gpu_checksum_xdr -- the proc checksum of messages serialized in
+//    XDR mode (HG_HAS_XDR, src/mercury_proc.h:110-122,147-160), where the
+//    buffer holds big-endian, 4-byte-rounded XDR but the checksum covers the
+//    host-order field values: a per-field schema says how to undo the XDR.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <type_traits>
 
 #include "crc_gpu_device.h"
 #include "gpu_host.h"
@@ -437,6 +442,114 @@ __global__ __launch_bounds__(256) void core_header_kernel(HdrArgs a) {
     }
 }
 
+// ------------------------------------------------------------------ XDR ----
+//
+// Under HG_HAS_XDR every typed field goes through xdr_<type>: RNDUP(sizeof)
+// bytes on the wire -- a 1-, 2- or 4-byte integer as one big-endian 32-bit
+// word (sign-extended for the signed types), an 8-byte integer as two
+// big-endian words, high first -- while HG_PROC_CHECKSUM_UPDATE hashes the
+// sizeof(type) bytes of the HOST variable (src/mercury_proc.h:110-122).  Byte
+// arrays go through xdr_opaque: the bytes, then zero pad to a multiple of 4,
+// with only the bytes hashed (:147-160).  hg_proc_save_ptr/restore_ptr regions
+// (bulk handles, src/mercury_proc_bulk.c:91-125) are raw at their exact size
+// (src/mercury_proc.c:277-335).  So a whole-buffer CRC is wrong in XDR mode;
+// this kernel walks a per-message field schema instead.  The hashed stream of
+// a little-endian host is, per field: the low `size` bytes of the decoded
+// integer in little-endian order, or the raw bytes of an opaque/raw field.
+//
+// One wave per message, the schema walk wave-uniform (the schema rides in the
+// kernel arguments).  The register L of the hashed stream (zero init, no
+// finalisation) is built field by field: an integer updates it byte by byte
+// from an LDS byte table; an opaque or raw field of n bytes is cut into 64
+// lane ranges hashed byte by byte, each shifted past the bytes after it
+// (Z^k from the base-16 digit tables) and XOR-reduced over the wave, then
+// L <- Z^n(L) ^ that.  CRC = L ^ Z^N(init) ^ xorout, N = hashed byte count.
+constexpr uint32_t kXdrMaxFields = 64;
+
+struct XdrArgs {
+    const uint8_t *buf;
+    const uint64_t *off;
+    uint64_t count;
+    void *out;
+    uint8_t *status;
+    const void *shift;
+    uint64_t rpoly, init, xorout;
+    uint32_t nf;
+    uint32_t kind[kXdrMaxFields], size[kXdrMaxFields];
+};
+
+template <int W>
+using xdr_reg_t = typename std::conditional<W == 32, uint32_t, uint64_t>::type;
+
+template <int W>
+__device__ __forceinline__ xdr_reg_t<W> xdr_shift(const void *sp, xdr_reg_t<W> x, uint64_t n) {
+    if constexpr (W == 32) return shift32(reinterpret_cast<const crc32_shift_pack_t *>(sp), x, n);
+    else return shift64(reinterpret_cast<const crc64_shift_pack_t *>(sp), x, n);
+}
+
+template <int W>
+__global__ __launch_bounds__(256) void xdr_kernel(XdrArgs a) {
+    using R = xdr_reg_t<W>;
+    __shared__ R tab[256];
+    {
+        R r = (R)threadIdx.x;  // byte table of the register form: Z^1 of the low byte
+        for (int k = 0; k < 8; k++) r = (r & 1u) ? (r >> 1) ^ (R)a.rpoly : r >> 1;
+        tab[threadIdx.x] = r;
+    }
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t nw = (uint64_t)gridDim.x * 4;
+    for (uint64_t m = uniform((uint32_t)(blockIdx.x * 4 + (threadIdx.x >> 6))); m < a.count; m += nw) {
+        uint64_t pos = a.off[m];
+        const uint64_t end = a.off[m + 1];
+        R acc = 0;
+        uint64_t N = 0, last = 0;
+        bool bad = end < pos;
+        for (uint32_t f = 0; f < a.nf && !bad; f++) {
+            const uint32_t kind = a.kind[f], sz = a.size[f];
+            if (kind == MCHECKSUM_XDR_SKIP_IF_ZERO) {
+                if (last == 0) f += sz;
+                continue;
+            }
+            if (kind == MCHECKSUM_XDR_INT) {
+                const uint32_t slot = sz <= 4 ? 4u : 8u;
+                if (end - pos < slot) {
+                    bad = true;
+                    break;
+                }
+                uint64_t v = 0;
+                for (uint32_t b = 0; b < slot; b++) v = v << 8 | a.buf[pos + b];
+                for (uint32_t b = 0; b < sz; b++) acc = (acc >> 8) ^ tab[(uint32_t)(acc ^ (R)(v >> (8 * b))) & 0xFFu];
+                last = sz == 8 ? v : v & ((1ull << (8 * sz)) - 1);
+                N += sz;
+                pos += slot;
+                continue;
+            }
+            const bool raw = kind == MCHECKSUM_XDR_RAW || kind == MCHECKSUM_XDR_RAW_LEN;
+            const uint64_t len = (kind == MCHECKSUM_XDR_OPAQUE_LEN || kind == MCHECKSUM_XDR_RAW_LEN) ? last : sz;
+            if (len > end - pos || (!raw && ((len + 3) & ~3ull) > end - pos)) {
+                bad = true;
+                break;
+            }
+            const uint64_t chunk = (len + 63) / 64;
+            const uint64_t lo = lane * chunk < len ? lane * chunk : len, hi = lo + chunk < len ? lo + chunk : len;
+            R p = 0;
+            for (uint64_t i = lo; i < hi; i++) p = (p >> 8) ^ tab[(uint32_t)(p ^ a.buf[pos + i]) & 0xFFu];
+            p = xdr_shift<W>(a.shift, p, len - hi);
+#pragma unroll
+            for (int k = 1; k < 64; k <<= 1) p ^= __shfl_xor(p, k, 64);
+            acc = xdr_shift<W>(a.shift, acc, len) ^ p;
+            N += len;
+            pos += raw ? len : (len + 3) & ~3ull;
+        }
+        if (lane == 0) {
+            const R crc = bad ? (R)0 : acc ^ xdr_shift<W>(a.shift, (R)a.init, N) ^ (R)a.xorout;
+            reinterpret_cast<R *>(a.out)[m] = crc;
+            if (a.status) a.status[m] = bad ? 1 : 0;
+        }
+    }
+}
+
 }  // namespace
 
 // ------------------------------------------------------------ host side ----
@@ -618,6 +731,57 @@ int mchecksum_gpu_verify_core_headers(const char *hash_method, int kind, const v
     hipLaunchKernelGGL(core_header_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_err(e, "core header kernel launch");
+    return MCHECKSUM_GPU_OK;
+}
+
+int mchecksum_gpu_checksum_xdr(const char *hash_method, const mchecksum_xdr_field_t *fields, size_t nfields,
+                               const void *dev_buf, const uint64_t *dev_msg_offsets, size_t count, void *dev_out,
+                               uint8_t *dev_status, void *stream) {
+    if ((nfields && !fields) || !dev_msg_offsets || (count && (!dev_buf || !dev_out)))
+        return set_err(MCHECKSUM_GPU_EINVAL, "NULL pointer argument");
+    if (nfields > kXdrMaxFields) return set_err(MCHECKSUM_GPU_EINVAL, "more than %u schema fields", kXdrMaxFields);
+    XdrArgs a{};
+    for (size_t f = 0; f < nfields; f++) {
+        const uint32_t k = fields[f].kind, z = fields[f].size;
+        const bool ok = (k == MCHECKSUM_XDR_INT && (z == 1 || z == 2 || z == 4 || z == 8)) ||
+                        k == MCHECKSUM_XDR_OPAQUE || k == MCHECKSUM_XDR_RAW || k == MCHECKSUM_XDR_OPAQUE_LEN ||
+                        k == MCHECKSUM_XDR_RAW_LEN || (k == MCHECKSUM_XDR_SKIP_IF_ZERO && z <= nfields - f - 1);
+        if (!ok) return set_err(MCHECKSUM_GPU_EINVAL, "schema field %zu: bad kind %u / size %u", f, k, z);
+        a.kind[f] = k;
+        a.size[f] = z;
+    }
+    int width = 0;
+    const int idx = gpu_model(hash_method, &width);
+    if (idx == -1) return set_err(MCHECKSUM_GPU_EMETHOD, "unknown hash method \"%s\"", hash_method ? hash_method : "(null)");
+    if (idx < 0) return set_err(MCHECKSUM_GPU_EMETHOD, "method \"%s\" has no GPU kernel (reflected 32/64-bit only)", hash_method);
+    if (!mchecksum_gpu_available()) return set_err(MCHECKSUM_GPU_ENODEV, "no HIP device");
+    DevCtx *c = nullptr;
+    const void *shift = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        int rc = device_ctx(&c);
+        if (rc) return rc;
+        rc = get_ext(c, idx, &shift);
+        if (rc) return rc;
+    }
+    if (count == 0) return MCHECKSUM_GPU_OK;
+    const mck_model_t &m = mck_models[idx];
+    a.buf = (const uint8_t *)dev_buf;
+    a.off = dev_msg_offsets;
+    a.count = count;
+    a.out = dev_out;
+    a.status = dev_status;
+    a.shift = shift;
+    a.rpoly = mck_reflect(m.poly, m.width);
+    a.init = mck_reflect(m.init, m.width);
+    a.xorout = m.xorout;
+    a.nf = (uint32_t)nfields;
+    uint64_t blocks = (count + 3) / 4;
+    if (blocks > (uint64_t)c->cus * 8) blocks = (uint64_t)c->cus * 8;
+    if (width == 32) hipLaunchKernelGGL(xdr_kernel<32>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
+    else hipLaunchKernelGGL(xdr_kernel<64>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_err(e, "XDR kernel launch");
     return MCHECKSUM_GPU_OK;
 }
 

@@ -303,6 +303,33 @@ def verify_core_headers(data: torch.Tensor, msg_offsets: torch.Tensor, kind: str
     return status, mism
 
 
+XDR_INT, XDR_OPAQUE, XDR_OPAQUE_LEN, XDR_RAW, XDR_RAW_LEN, XDR_SKIP_IF_ZERO = 0, 1, 2, 3, 4, 5
+
+
+def checksum_xdr(method: str, data: torch.Tensor, msg_offsets: torch.Tensor, schema, status: bool = False,
+                 stream=None, offsets_host=None):
+    """Proc checksum of messages serialized in XDR mode (include/mchecksum_gpu.h,
+    mchecksum_gpu_checksum_xdr): schema = [(kind, size), ...] with the XDR_*
+    kinds.  Returns the CRC tensor, or (CRCs, status) with status=True
+    (status 1 = the schema runs past the message)."""
+    from ._lib import XdrField
+    _check_device_u8(data, "data")
+    _check_offsets(data, msg_offsets, offsets_host)
+    _same_device(data, msg_offsets=msg_offsets)
+    count = msg_offsets.numel() - 1
+    fields = (XdrField * max(1, len(schema)))(*[XdrField(int(k), int(z)) for k, z in schema])
+    out = torch.empty(max(count, 0), dtype=out_dtype(method), device=data.device)
+    st = torch.ones(max(count, 0), dtype=torch.uint8, device=data.device) if status else None
+    with _on(data):
+        rc = _lib().mchecksum_gpu_checksum_xdr(method.encode(), fields, len(schema), data.data_ptr(),
+                                               msg_offsets.data_ptr(), count, out.data_ptr(),
+                                               st.data_ptr() if st is not None else None,
+                                               _stream_handle(stream, data.device))
+    if rc != 0:
+        _err(rc, "mchecksum_gpu_checksum_xdr")
+    return (out, st) if status else out
+
+
 def fill_splitmix(t: torch.Tensor, seed: int, first_word: int = 0, stream=None) -> torch.Tensor:
     """Fill a device tensor with the synthetic payload bytes of SURVEY.md 8(d)."""
     _check_device_u8(t, "tensor")

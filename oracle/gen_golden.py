@@ -112,6 +112,17 @@ def core_header_fixtures():
     return out
 
 
+def test_proc_xdr():
+    """The same payloads serialized with MERCURY_USE_XDR (src/mercury_proc.h:
+    110-122,147-160): u8/u16/u32 as 4-byte big-endian words, u64 as 8; the
+    string's bytes through xdr_opaque (zero pad to 4), its two u8 flags as
+    4-byte words.  Schema kinds: include/mchecksum_gpu.h MCHECKSUM_XDR_*."""
+    st = [(O.XDR_INT, 1), (O.XDR_INT, 2), (O.XDR_INT, 4), (O.XDR_INT, 8)]
+    sg = [(O.XDR_INT, 8), (O.XDR_SKIP_IF_ZERO, 3), (O.XDR_OPAQUE_LEN, 0), (O.XDR_INT, 1), (O.XDR_INT, 1)]
+    return {"uint_struct": (st, O.xdr_encode(st, [1, 2, 3, 4])),
+            "string_hello": (sg, O.xdr_encode(sg, [6, b"Hello\x00", 0, 0]))}
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     cat = {k: {"width": w, "poly": hex(p), "refin": ri, "refout": ro, "init": hex(i), "xorout": hex(x),
@@ -123,14 +134,20 @@ def main():
               open(os.path.join(OUT, "rfc3720.json"), "w"), indent=1)
 
     tp = {}
+    xdr = test_proc_xdr()
     for name, (img, fields) in test_proc_images().items():
         c32 = O.crc("crc32c", img)
         assert c32 == O.crc("crc32c", img, variant="sse42")
+        schema, wire = xdr[name]
+        assert O.xdr_hashed_stream(schema, wire) == img  # XDR mode hashes the same host values
         tp[name] = {"hex": img.hex(), "field_sizes": fields,
-                    **{m: hex(O.crc(m, img)) for m in METHODS}}
+                    **{m: hex(O.crc(m, img)) for m in METHODS},
+                    "xdr_hex": wire.hex(), "xdr_schema": [list(f) for f in schema]}
     json.dump({"source": "Testing/unit/hg/test_proc.c:186-227 payload images (non-XDR, little-endian)",
                "pinned": {"crc32c": "RFC 3720 standard + SSE4.2", "crc64": "parity unpinned (CRC-64/XZ default)",
                           "crc16": "parity unpinned (CRC-16/T10-DIF default)"},
+               "xdr": "xdr_hex: the payload as MERCURY_USE_XDR serializes it (src/mercury_proc.h:110-160); "
+                      "its proc checksum is the CRC of hex (the host-order values)",
                "payloads": tp}, open(os.path.join(OUT, "test_proc.json"), "w"), indent=1)
 
     lengths = [0, 1, 3, 7, 8, 9, 63, 64, 65, 4095, 4096, 4097, 65535, 65536]

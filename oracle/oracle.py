@@ -162,3 +162,72 @@ def splitmix_batch_fixed(method, seed, stride, length, first, count, variant="ta
     if rc:
         raise RuntimeError("oracle_splitmix_batch_fixed failed")
     return out
+
+
+# ------------------------------------------------------------------- XDR ----
+# CPU restatement of what Mercury's proc layer hashes in XDR mode
+# (HG_HAS_XDR; /root/reference/src/mercury_proc.h:110-122 HG_PROC_TYPE,
+# :147-160 HG_PROC_BYTES; save/restore_ptr src/mercury_proc.c:277-335): each
+# typed field occupies RNDUP(sizeof(type)) big-endian wire bytes (xdr_<type>;
+# 1/2/4-byte integers as one 32-bit word, 8-byte ones as two, high first) but
+# the checksum is updated with the sizeof(type) bytes of the host variable --
+# little-endian on this host; byte arrays are xdr_opaque (bytes + zero pad to
+# 4), hashed without the pad; save_ptr regions are raw and exact.  Schema kinds
+# as include/mchecksum_gpu.h (MCHECKSUM_XDR_*).
+XDR_INT, XDR_OPAQUE, XDR_OPAQUE_LEN, XDR_RAW, XDR_RAW_LEN, XDR_SKIP_IF_ZERO = 0, 1, 2, 3, 4, 5
+
+
+def xdr_encode(schema, values) -> bytes:
+    """XDR wire image of one message: values[i] is the integer (INT) or the
+    bytes (OPAQUE*/RAW*) of the i-th non-SKIP field that is present."""
+    out, vals, last, f = bytearray(), list(values), None, 0
+    while f < len(schema):
+        kind, size = schema[f]
+        if kind == XDR_SKIP_IF_ZERO:
+            if last == 0:
+                f += size
+            f += 1
+            continue
+        v = vals.pop(0)
+        if kind == XDR_INT:
+            slot = 4 if size <= 4 else 8
+            # xdr_<type>: the value as a 32-bit (signed types sign-extended)
+            # or 64-bit big-endian integer
+            out += (int(v) & ((1 << (8 * slot)) - 1)).to_bytes(slot, "big")
+            last = int(v) & ((1 << (8 * size)) - 1)
+        else:
+            b = bytes(v)
+            out += b
+            if kind in (XDR_OPAQUE, XDR_OPAQUE_LEN):
+                out += b"\0" * (-len(b) % 4)
+        f += 1
+    return bytes(out)
+
+
+def xdr_hashed_stream(schema, msg: bytes):
+    """The bytes Mercury's XDR-mode proc checksum covers for one message, or
+    None when the schema runs past the message."""
+    pos, last, out, f = 0, 0, bytearray(), 0
+    while f < len(schema):
+        kind, size = schema[f]
+        f += 1
+        if kind == XDR_SKIP_IF_ZERO:
+            if last == 0:
+                f += size
+            continue
+        if kind == XDR_INT:
+            slot = 4 if size <= 4 else 8
+            if pos + slot > len(msg):
+                return None
+            v = int.from_bytes(msg[pos:pos + slot], "big")
+            out += (v & ((1 << (8 * size)) - 1)).to_bytes(size, "little")
+            last = v & ((1 << (8 * size)) - 1)
+            pos += slot
+            continue
+        n = last if kind in (XDR_OPAQUE_LEN, XDR_RAW_LEN) else size
+        wire = n if kind in (XDR_RAW, XDR_RAW_LEN) else n + (-n % 4)
+        if pos + wire > len(msg):
+            return None
+        out += msg[pos:pos + n]
+        pos += wire
+    return bytes(out)

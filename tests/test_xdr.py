@@ -1,0 +1,138 @@
+"""XDR-mode proc checksum (include/mchecksum_gpu.h,
+mchecksum_gpu_checksum_xdr).
+
+In a Mercury built with MERCURY_USE_XDR the proc buffer holds XDR (integers
+big-endian in 4/8-byte slots, byte arrays zero-padded to 4) while the
+checksum covers the host-order values (/root/reference/src/mercury_proc.h:
+110-122,147-160).  CPU tests pin the oracle's restatement (oracle.xdr_*)
+on test_proc's two payloads; GPU tests compare the batch kernel with
+oracle.crc(method, xdr_hashed_stream(...)) on the fixtures and on random
+messages of every field kind."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+GOLD = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "test_proc.json")))
+
+
+def test_xdr_images_hash_the_host_values(oracle_mod):
+    """test_proc's struct and string in XDR: the hashed stream is exactly the
+    non-XDR image, so the checksum value is the same in both builds."""
+    O = oracle_mod
+    for name, e in GOLD["payloads"].items():
+        schema = [tuple(f) for f in e["xdr_schema"]]
+        wire = bytes.fromhex(e["xdr_hex"])
+        assert O.xdr_encode(schema, _values(O, name)) == wire
+        assert O.xdr_hashed_stream(schema, wire) == bytes.fromhex(e["hex"])
+        for m in ("crc32c", "crc64"):
+            assert O.crc(m, O.xdr_hashed_stream(schema, wire)) == int(e[m], 16)
+        assert O.xdr_hashed_stream(schema, wire[:-1]) is None  # truncated
+
+
+def _values(O, name):
+    return [1, 2, 3, 4] if name == "uint_struct" else [6, b"Hello\x00", 0, 0]
+
+
+# ----------------------------------------------------------------- GPU ----
+
+def _schemas(O):
+    I, OP, OPL, RAW, RAWL, SKIP = (O.XDR_INT, O.XDR_OPAQUE, O.XDR_OPAQUE_LEN, O.XDR_RAW, O.XDR_RAW_LEN,
+                                   O.XDR_SKIP_IF_ZERO)
+    return {
+        # hg_perf_proc_iovec (Testing/perf/hg/mercury_perf.c:897-923): u32 length, raw bytes
+        "iovec": [(I, 4), (OPL, 0)],
+        # a struct with every integer width, an hg_string_t, a bulk handle
+        # (u64 serialize size + save_ptr region) and a fixed opaque
+        "mixed": [(I, 1), (I, 2), (I, 4), (I, 8), (I, 8), (SKIP, 3), (OPL, 0), (I, 1), (I, 1),
+                  (I, 8), (RAWL, 0), (OP, 7), (RAW, 5), (I, 2)],
+    }
+
+
+def _random_values(rng, schema, O, max_len):
+    vals, last, f = [], None, 0
+    while f < len(schema):
+        kind, size = schema[f]
+        if kind == O.XDR_SKIP_IF_ZERO:
+            if last == 0:
+                f += size
+            f += 1
+            continue
+        nxt = schema[f + 1][0] if f + 1 < len(schema) else None
+        if kind == O.XDR_INT:
+            if nxt in (O.XDR_OPAQUE_LEN, O.XDR_RAW_LEN) or (nxt == O.XDR_SKIP_IF_ZERO):
+                v = int(rng.choice([0, 1, 3, 4, 5, 63, 64, 65, 1000, int(rng.integers(0, max_len))]))
+            else:
+                v = int(rng.integers(-(1 << (8 * size - 1)), 1 << (8 * size - 1)))  # signed range, sign-extended
+            vals.append(v)
+            last = v & ((1 << (8 * size)) - 1)
+        else:
+            n = last if kind in (O.XDR_OPAQUE_LEN, O.XDR_RAW_LEN) else size
+            vals.append(rng.integers(0, 256, n, dtype=np.uint8).tobytes())
+        f += 1
+    return vals
+
+
+def _run(gpu, method, msgs, schema, status=False):
+    import torch
+    off = np.zeros(len(msgs) + 1, dtype=np.int64)
+    off[1:] = np.cumsum([len(m) for m in msgs])
+    blob = b"".join(msgs)
+    data = torch.zeros(len(blob) + 64, dtype=torch.uint8, device="cuda")
+    if blob:
+        data[:len(blob)].copy_(torch.from_numpy(np.frombuffer(blob, dtype=np.uint8).copy()))
+    r = gpu.checksum_xdr(method, data, torch.from_numpy(off).cuda(), schema, status=status, offsets_host=off)
+    if status:
+        return gpu.as_unsigned(r[0]), r[1].cpu().numpy()
+    return gpu.as_unsigned(r)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("method", ["crc32c", "crc64"])
+def test_gpu_xdr_test_proc_fixtures(gpu, method):
+    for name, e in GOLD["payloads"].items():
+        schema = [tuple(f) for f in e["xdr_schema"]]
+        got = _run(gpu, method, [bytes.fromhex(e["xdr_hex"])] * 3, schema)
+        assert got.tolist() == [int(e[method], 16)] * 3, name
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("method", ["crc32c", "crc64"])
+@pytest.mark.parametrize("kind", ["iovec", "mixed"])
+def test_gpu_xdr_random_messages(gpu, oracle_mod, method, kind):
+    O = oracle_mod
+    schema = _schemas(O)[kind]
+    rng = np.random.default_rng(17 if kind == "iovec" else 18)
+    msgs = [O.xdr_encode(schema, _random_values(rng, schema, O, 70000 if i % 97 == 0 else 3000))
+            for i in range(700)]
+    got = _run(gpu, method, msgs, schema)
+    want = [O.crc(method, O.xdr_hashed_stream(schema, m)) for m in msgs]
+    assert got.tolist() == want
+
+
+@pytest.mark.gpu
+def test_gpu_xdr_truncated_messages_are_flagged(gpu, oracle_mod):
+    O = oracle_mod
+    schema = _schemas(O)["mixed"]
+    rng = np.random.default_rng(5)
+    msgs = [O.xdr_encode(schema, _random_values(rng, schema, O, 500)) for _ in range(40)]
+    cut = {3: 1, 10: 5, 20: len(msgs[20]) // 2}
+    msgs = [m[:len(m) - cut[i]] if i in cut else m for i, m in enumerate(msgs)]
+    got, st = _run(gpu, "crc32c", msgs, schema, status=True)
+    assert sorted(np.nonzero(st)[0].tolist()) == sorted(cut)
+    for i, m in enumerate(msgs):
+        if i not in cut:
+            assert int(got[i]) == O.crc("crc32c", O.xdr_hashed_stream(schema, m))
+
+
+@pytest.mark.gpu
+def test_gpu_xdr_rejects_bad_schemas(gpu):
+    import torch
+    data = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    offs = torch.tensor([0, 8], dtype=torch.int64, device="cuda")
+    for bad in ([(0, 3)], [(9, 1)], [(5, 2), (0, 4)], [(0, 4)] * 65):
+        with pytest.raises(gpu.GpuChecksumError):
+            gpu.checksum_xdr("crc32c", data, offs, bad)
+    with pytest.raises(gpu.GpuChecksumError):
+        gpu.checksum_xdr("crc16", data, offs, [(0, 4)])
