@@ -162,7 +162,13 @@ struct BatchArgs {
     // optional caller word (mchecksum_gpu_set_error_word): +1 when this launch
     // could not hash every payload (fail-closed report for checksum modes)
     uint32_t *err_word;
+    // split CRC-64 pieces (crc64_batch_kernel<..., SPLIT>): each payload is
+    // 2^split_log2 pieces of kSplitBytes, recombined with the Z^n shift pack
+    const void *shift;
+    uint32_t split_log2;
 };
+// Piece size of a split payload: 256 KiB = 256 steps of the G = 64 loop.
+constexpr uint64_t kSplitBytes = 256u << 10;
 
 // ------------------------------------------------------------ work queue --
 // Dynamic distribution of payloads over waves.  With a static assignment the
@@ -1101,6 +1107,36 @@ __global__ __launch_bounds__(kBlk32<LIGHT>, 1) void crc32c_batch_kernel(BatchArg
     MCK_STAMP(wave, 2);
 }
 
+// Z^n(x) from the base-16 digit tables; n and x are wave-uniform on the chunk
+// paths (mchecksum_gpu_ext.hip) and the split CRC-64 pieces below, so the table words come through the scalar cache.
+__device__ __forceinline__ uint32_t shift32(const crc32_shift_pack_t *sp, uint32_t x, uint64_t n) {
+    for (int k = 0; n; k++, n >>= 4) {
+        const uint32_t d = (uint32_t)(n & 15u);
+        if (d) {
+            const uint32_t *t = &sp->op[k][d - 1][0][0];
+            uint32_t r = 0;
+#pragma unroll
+            for (int h = 0; h < 8; h++) r ^= t[h * 16 + ((x >> (4 * h)) & 15u)];
+            x = r;
+        }
+    }
+    return x;
+}
+
+__device__ __forceinline__ uint64_t shift64(const crc64_shift_pack_t *sp, uint64_t x, uint64_t n) {
+    for (int k = 0; n; k++, n >>= 4) {
+        const uint32_t d = (uint32_t)(n & 15u);
+        if (d) {
+            const uint64_t *t = &sp->op[k][d - 1][0][0];
+            uint64_t r = 0;
+#pragma unroll
+            for (int h = 0; h < 16; h++) r ^= t[h * 16 + ((x >> (4 * h)) & 15u)];
+            x = r;
+        }
+    }
+    return x;
+}
+
 // ----------------------------------------------------------------- CRC-64 --
 
 __device__ __forceinline__ uint64_t xor3_64(uint64_t a, uint64_t b, uint64_t c) {
@@ -1489,19 +1525,28 @@ __device__ __forceinline__ uint64_t payload64_g64(const uint8_t *lds, const crc6
     return x;
 }
 
-template <int LOG2G, int MODE, bool VERIFY, bool NT>
+// SPLIT (aligned batches of large payloads, G = 64): a unit is one
+// kSplitBytes piece q of payload p, so the work queue balances pieces instead
+// of whole 1 MiB payloads (one per wave at C3's shape: the slowest XCD set the
+// launch time).  By linearity the payload's register is the XOR over pieces of
+// Z^(bytes after piece q)(L_q), L_0 carrying the initial value; each piece
+// adds its term (and piece 0 the final XOR) to out[p] with a 64-bit atomic
+// XOR, into an output the host zeroed before the launch.
+template <int LOG2G, int MODE, bool VERIFY, bool NT, bool SPLIT = false>
 __global__ __launch_bounds__(kBlk64<MODE>, kWpe64<MODE>) void crc64_batch_kernel(BatchArgs a) {
     using S = Shape<64, MODE>;
     constexpr int kWPB = S::block / 64;
     __shared__ __attribute__((aligned(16))) uint8_t lds[S::lds64_bytes];
     const crc64_gpu_pack_t *pk = reinterpret_cast<const crc64_gpu_pack_t *>(a.pack);
     constexpr int PPW = 64 >> LOG2G;
-    const uint64_t units = MODE == kOffsets ? a.count : (a.count + PPW - 1) / PPW;
+    const uint64_t units = MODE == kOffsets ? a.count : SPLIT ? a.count << a.split_log2 : (a.count + PPW - 1) / PPW;
     __shared__ WgQueue wgq;
-    constexpr bool DYN = dyn_policy(64, MODE, NT, false);
+    constexpr bool DYN = dyn_policy(64, MODE, NT, false) || SPLIT;
+    MCK_STAMP(blockIdx.x * kWPB + (threadIdx.x >> 6), 0);
     if (DYN && threadIdx.x == 0) wg_queue_init(&wgq, a.queue, units, a.own);
     fill_lds64<S::block, S::ops_mode>(lds, pk);
     __syncthreads();
+    MCK_STAMP(blockIdx.x * kWPB + (threadIdx.x >> 6), 1);
 
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t gl = lane & ((1u << LOG2G) - 1u), grp = lane >> LOG2G;
@@ -1527,6 +1572,24 @@ __global__ __launch_bounds__(kBlk64<MODE>, kWpe64<MODE>) void crc64_batch_kernel
         if (for_each_unit<true>(&wgq, a.queue, units, wave, nw, a.own, one)) fail_closed<VERIFY>(a);
         return;
     }
+    if constexpr (SPLIT) {
+        static_assert(LOG2G == 6 && MODE == kFixedAligned && !VERIFY, "split pieces: aligned G = 64 checksums");
+        const uint32_t sl = a.split_log2, pieces = 1u << sl;
+        const crc64_shift_pack_t *sp = reinterpret_cast<const crc64_shift_pack_t *>(a.shift);
+        const bool faulted = for_each_unit<true>(&wgq, a.queue, units, wave, nw, a.own, [&](uint64_t u) {
+            const uint64_t p = u >> sl;
+            const uint32_t q = (uint32_t)u & (pieces - 1);
+            const uint64_t x = payload64_aligned<6, NT, S::ops_global>(
+                lds, pk, a.base + p * a.stride + (uint64_t)q * kSplitBytes, (uint32_t)(kSplitBytes >> 10), gl, lc,
+                q == 0 ? pk->init : 0ull);
+            if (gl == 0) {
+                const uint64_t t = shift64(sp, x, (uint64_t)(pieces - 1 - q) * kSplitBytes) ^ (q == 0 ? xorout : 0ull);
+                atomicXor(reinterpret_cast<unsigned long long *>(a.out) + p, (unsigned long long)t);
+            }
+        });
+        if (faulted) fail_closed<false>(a);
+        return;
+    }
     const bool faulted = for_each_unit<DYN>(&wgq, a.queue, units, wave, nw, a.own, [&](uint64_t u) {
         const uint64_t p = u * PPW + grp;
         const bool act = p < a.count;
@@ -1539,6 +1602,7 @@ __global__ __launch_bounds__(kBlk64<MODE>, kWpe64<MODE>) void crc64_batch_kernel
         if (act && gl == 0) emit<uint64_t, VERIFY>(a, p, x ^ xorout);
     });
     if (faulted) fail_closed<VERIFY>(a);
+    MCK_STAMP(blockIdx.x * kWPB + (threadIdx.x >> 6), 2);
 }
 
 }  // namespace

@@ -52,6 +52,10 @@ int gpu_model(const char *method, int *width);
 int device_ctx(DevCtx **out);
 // Model + device context + table pack for lanes-per-payload 2^log2g (takes g_mu).
 int prologue(const char *method, int log2g, int *width, DevCtx **c, const void **pack);
+// Per-device, per-model extension tables (mchecksum_gpu_ext.hip): the
+// Z^n shift pack of a 32/64-bit model, the byte table of a 16-bit one
+// (caller holds g_mu).
+int get_ext(DevCtx *c, int idx, const void **out);
 // Work-queue slot for one launch of a throughput (non-light) batch kernel on
 // `stream`; *own = 1 when the launch must claim it on the device.
 unsigned long long *queue_slot(DevCtx *c, void *stream, uint32_t *own);

@@ -339,8 +339,24 @@ int do_offsets(const char *method, const void *base, const uint64_t *offsets, si
     return launch(k, a, grid_for(c, count, k), stream);
 }
 
-int launch_fixed(DevCtx *c, const void *pack, int width, int lg, const void *dev_base, size_t stride, size_t len,
-                 size_t count, void *dev_out, void *stream, bool light) {
+// Large aligned CRC-64 payloads go to the work queue as kSplitBytes pieces
+// (crc64_batch_kernel<..., SPLIT>) once the batch is big enough for the
+// non-temporal path; MCHECKSUM_GPU_SPLIT=0/1 overrides.
+bool use_split(int width, int lg, bool aligned, bool nt, size_t len, size_t stride) {
+    const char *env = getenv("MCHECKSUM_GPU_SPLIT");
+    if (env && env[0] && env[0] != '1') return false;
+    const bool shape = width == 64 && lg == CRC_GPU_MAX_LOG2G && aligned && len % kSplitBytes == 0 &&
+                       len / kSplitBytes >= 2 && len / kSplitBytes <= 64 && ((len / kSplitBytes) & (len / kSplitBytes - 1)) == 0 &&
+                       stride % 16 == 0;
+    if (env && env[0] == '1') return shape;
+#ifndef MCK_SPLIT64
+#define MCK_SPLIT64 1
+#endif
+    return MCK_SPLIT64 && shape && nt;
+}
+
+int launch_fixed(DevCtx *c, int idx, const void *pack, int width, int lg, const void *dev_base, size_t stride,
+                 size_t len, size_t count, void *dev_out, void *stream, bool light) {
     const uint64_t step = 16ull << lg;
     // The aligned path needs whole steps and K = len/step a multiple of the
     // load ring depth; everything else takes the generic path.
@@ -355,6 +371,27 @@ int launch_fixed(DevCtx *c, const void *pack, int width, int lg, const void *dev
     a.pack = pack;
     a.err_word = t_err_word;
     const bool nt = !light && use_nt((uint64_t)len * count);
+    uint32_t sl = 0;
+    while ((kSplitBytes << sl) < len && sl < 63) sl++;
+    if (use_split(width, lg, aligned, nt, len, count > 1 ? stride : 16) && ((uint64_t)count << sl) <= kMaxUnits) {
+        const void *shift = nullptr;
+        {
+            std::lock_guard<std::mutex> lk(g_mu);
+            int rc = get_ext(c, idx, &shift);
+            if (rc) return rc;
+        }
+        a.shift = shift;
+        a.split_log2 = sl;
+        a.queue = queue_slot(c, stream, &a.own);
+        // the pieces XOR their terms into out[]: zero it first (in stream order)
+        hipError_t e = hipMemsetAsync(dev_out, 0, count * sizeof(uint64_t), (hipStream_t)stream);
+        if (e != hipSuccess) return hip_err(e, "output zeroing");
+        const KLaunch k = nt ? KLaunch{crc64_batch_kernel<6, kFixedAligned, false, true, true>, Shape<64, kFixedAligned>::block,
+                                       Shape<64, kFixedAligned>::blocks_per_cu}
+                             : KLaunch{crc64_batch_kernel<6, kFixedAligned, false, false, true>, Shape<64, kFixedAligned>::block,
+                                       Shape<64, kFixedAligned>::blocks_per_cu};
+        return launch(k, a, grid_for(c, (uint64_t)count << sl, k), stream);
+    }
     const KLaunch k = width == 32 ? pick_fixed<32>(lg, aligned, nt, light) : pick_fixed<64>(lg, aligned, nt, false);
     const uint64_t ppw = 64u >> lg;
     if (dyn_policy(width, aligned ? kFixedAligned : kFixedGeneric, nt, light)) a.queue = queue_slot(c, stream, &a.own);
@@ -426,7 +463,8 @@ int mchecksum_gpu_checksum_fixed(const char *hash_method, const void *dev_base, 
         int rc = prologue(hash_method, lg, &width, &c, &pack);
         if (rc) return rc;
         if (count == 0) return MCHECKSUM_GPU_OK;
-        return launch_fixed(c, pack, width, lg, dev_base, stride, len, count, dev_out, stream, true);
+        return launch_fixed(c, gpu_model(hash_method, &width), pack, width, lg, dev_base, stride, len, count, dev_out,
+                            stream, true);
     }
     const int lg = choose_log2g(len);
     DevCtx *c = nullptr;
@@ -434,7 +472,8 @@ int mchecksum_gpu_checksum_fixed(const char *hash_method, const void *dev_base, 
     int rc = prologue(hash_method, lg, &width, &c, &pack);
     if (rc) return rc;
     if (count == 0) return MCHECKSUM_GPU_OK;
-    return launch_fixed(c, pack, width, lg, dev_base, stride, len, count, dev_out, stream, false);
+    return launch_fixed(c, gpu_model(hash_method, &width), pack, width, lg, dev_base, stride, len, count, dev_out,
+                        stream, false);
 }
 
 int mchecksum_gpu_checksum_offsets(const char *hash_method, const void *dev_base, const uint64_t *dev_offsets,

@@ -198,36 +198,6 @@ __global__ __launch_bounds__(kScanThreads) void seg_scan_down(const uint64_t *le
     }
 }
 
-// Z^n(x) from the base-16 digit tables; n and x are wave-uniform on the chunk
-// path, so the table words come through the scalar cache.
-__device__ __forceinline__ uint32_t shift32(const crc32_shift_pack_t *sp, uint32_t x, uint64_t n) {
-    for (int k = 0; n; k++, n >>= 4) {
-        const uint32_t d = (uint32_t)(n & 15u);
-        if (d) {
-            const uint32_t *t = &sp->op[k][d - 1][0][0];
-            uint32_t r = 0;
-#pragma unroll
-            for (int h = 0; h < 8; h++) r ^= t[h * 16 + ((x >> (4 * h)) & 15u)];
-            x = r;
-        }
-    }
-    return x;
-}
-
-__device__ __forceinline__ uint64_t shift64(const crc64_shift_pack_t *sp, uint64_t x, uint64_t n) {
-    for (int k = 0; n; k++, n >>= 4) {
-        const uint32_t d = (uint32_t)(n & 15u);
-        if (d) {
-            const uint64_t *t = &sp->op[k][d - 1][0][0];
-            uint64_t r = 0;
-#pragma unroll
-            for (int h = 0; h < 16; h++) r ^= t[h * 16 + ((x >> (4 * h)) & 15u)];
-            x = r;
-        }
-    }
-    return x;
-}
-
 // (readfirstlane returns int: cast through uint32_t so nothing sign-extends)
 __device__ __forceinline__ uint32_t uniform(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ uint64_t uniform(uint64_t v) {
@@ -558,7 +528,7 @@ namespace mck {
 
 // Per-device, per-model extension tables (shift pack for 32/64-bit models,
 // byte table for 16-bit ones), built and uploaded once under g_mu.
-static int get_ext(DevCtx *c, int idx, const void **out) {
+int get_ext(DevCtx *c, int idx, const void **out) {
     if (c->ext[idx]) {
         *out = c->ext[idx];
         return 0;

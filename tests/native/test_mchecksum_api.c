@@ -6,6 +6,7 @@
  *   "send" (memcpy), decode with the same per-field updates, verify with memcmp
  *   (hg_proc_checksum_verify, src/mercury_proc.c:433-472).
  * Adds what test_proc lacks: the pinned CRC-32C value of the encoded bytes,
+ * the save_ptr/restore_ptr pattern of bulk-handle procs (src/mercury_proc_bulk.c),
  * a corrupted-transfer case, every method's size, destroy(NULL), and distinct
  * objects used concurrently from 8 threads (Mercury's progress + handler
  * threads).  Built plain, with ASan+UBSan and with TSan (tests/test_native_api.py).
@@ -137,6 +138,81 @@ test_proc_string(void)
     mchecksum_destroy(p.ck);
 }
 
+/* hg_proc_save_ptr / hg_proc_restore_ptr as hg_proc_hg_bulk_t uses them
+ * (src/mercury_proc_bulk.c:82-93 encode, :111-125 decode;
+ * src/mercury_proc.c:277-335): save_ptr reserves buf_size bytes WITHOUT
+ * hashing, the serializer fills them, restore_ptr hashes that same region.
+ * The proc checksum must still equal one CRC over buf[0 : size_used) -- the
+ * invariant the whole-buffer GPU batch entry points rely on. */
+static unsigned char *
+proc_save_ptr(struct proc *p, size_t n)
+{
+    unsigned char *r = p->ptr;
+    p->ptr += n;
+    return r;
+}
+
+static void
+proc_restore_ptr(struct proc *p, const void *data, size_t n)
+{
+    mchecksum_update(p->ck, data, n);
+}
+
+static void
+test_proc_bulk_save_restore(void)
+{
+    struct proc p;
+    unsigned char in_buf[512] = {0}, out_buf[512] = {0}, sent[4];
+    uint8_t flags = 3;
+    uint64_t buf_size = 77, got_size = 0;
+    uint32_t whole = 0, h = 0;
+    size_t used, i;
+    unsigned char *region;
+    mchecksum_object_t c = MCHECKSUM_OBJECT_NULL;
+
+    CHECK(mchecksum_init("crc32c", &p.ck) == 0, "init");
+    p.hash_size = 4;
+    proc_reset(&p, in_buf, 1);
+    proc_bytes(&p, &flags, 1);          /* a field before the handle */
+    proc_bytes(&p, &buf_size, 8);       /* hg_proc_uint64_t(proc, &buf_size) */
+    region = proc_save_ptr(&p, buf_size);
+    for (i = 0; i < buf_size; i++)      /* HG_Bulk_serialize(buf, buf_size, ...) */
+        region[i] = (unsigned char) (i * 37 + 11);
+    proc_restore_ptr(&p, region, buf_size);
+    proc_bytes(&p, &flags, 1);          /* and one after it */
+    proc_flush(&p);
+    used = (size_t) (p.ptr - p.buf);
+    memcpy(sent, p.hash, 4);
+    memcpy(&h, p.hash, 4);
+    mchecksum_init("crc32c", &c);
+    mchecksum_update(c, in_buf, used);  /* what a whole-buffer batch kernel hashes */
+    mchecksum_get(c, &whole, 4, MCHECKSUM_FINALIZE);
+    mchecksum_destroy(c);
+    CHECK(used == 1 + 8 + 77 + 1, "size_used");
+    CHECK(h == whole, "save_ptr/restore_ptr checksum == CRC of buf[0:size_used)");
+
+    memcpy(out_buf, in_buf, used);      /* the receiver: decode, save_ptr, restore_ptr, verify */
+    proc_reset(&p, out_buf, 0);
+    proc_bytes(&p, &flags, 1);
+    proc_bytes(&p, &got_size, 8);
+    region = proc_save_ptr(&p, got_size);
+    proc_restore_ptr(&p, region, got_size);
+    proc_bytes(&p, &flags, 1);
+    proc_flush(&p);
+    CHECK(got_size == 77 && memcmp(sent, p.hash, 4) == 0, "decode side verifies");
+
+    out_buf[40] ^= 1;                   /* a bit flipped inside the saved region */
+    proc_reset(&p, out_buf, 0);
+    proc_bytes(&p, &flags, 1);
+    proc_bytes(&p, &got_size, 8);
+    region = proc_save_ptr(&p, got_size);
+    proc_restore_ptr(&p, region, got_size);
+    proc_bytes(&p, &flags, 1);
+    proc_flush(&p);
+    CHECK(memcmp(sent, p.hash, 4) != 0, "corruption in the saved region detected");
+    mchecksum_destroy(p.ck);
+}
+
 static void
 test_methods_and_edges(void)
 {
@@ -235,6 +311,7 @@ main(void)
 {
     test_proc_uint();
     test_proc_string();
+    test_proc_bulk_save_restore();
     test_methods_and_edges();
     test_threads();
     if (failures) {

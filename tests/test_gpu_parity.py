@@ -237,3 +237,24 @@ def test_gpu_matches_streaming_api(gpu, oracle_mod):
         for a, b in [(0, 1), (1, 9), (9, 4096), (4096, 20000)]:  # per-field style updates
             c.update(host[a:b].tobytes())
         assert c.get() == got
+
+
+@pytest.mark.parametrize("count,length,extra", [(37, 512 << 10, 0), (5, 2 << 20, 4096), (3, 16 << 20, 16),
+                                                (1, 1 << 20, 0), (9, 1 << 20, 0)])
+def test_crc64_split_pieces(gpu, oracle_mod, monkeypatch, count, length, extra):
+    """CRC-64 payloads of whole 256 KiB pieces go to the work queue piece by
+    piece and are recombined with Z^n shifts (crc64_batch_kernel<..., SPLIT>):
+    forced on with MCHECKSUM_GPU_SPLIT=1 at these small sizes, equal to the
+    oracle and to the unsplit kernel (MCHECKSUM_GPU_SPLIT=0)."""
+    import torch
+    stride = length + extra
+    host = oracle_mod.splitmix_bytes(stride * (count - 1) + length, 0x5B17 + count)
+    dev = _dev_bytes(torch, host)
+    want = oracle_mod.batch_fixed("crc64", host, stride, length, count, nthreads=8)
+    stale = torch.full((count,), -1, dtype=torch.int64, device="cuda")  # the split path zeroes out[] itself
+    monkeypatch.setenv("MCHECKSUM_GPU_SPLIT", "1")
+    got = gpu.as_unsigned(gpu.checksum_fixed("crc64", dev, length, count=count, stride=stride, out=stale))
+    monkeypatch.setenv("MCHECKSUM_GPU_SPLIT", "0")
+    plain = gpu.as_unsigned(gpu.checksum_fixed("crc64", dev, length, count=count, stride=stride))
+    assert np.array_equal(got.astype(np.uint64), want)
+    assert np.array_equal(plain.astype(np.uint64), want)
