@@ -430,7 +430,7 @@ def cpu_baseline(method, seed, length, offsets_host, got, budget_s, samples, seg
     affinity = len(os.sched_getaffinity(0))
     quota = _cpu_quota()
     threads = max(1, min(256, affinity, int(quota[0]) if quota else affinity))
-    variant = "sse42" if method == "crc32c" else "table"
+    variant = "sse42" if method == "crc32c" else "slice8"
     slots = None
     if segments:
         from mercury_amd.workload import segment_slots
@@ -468,13 +468,13 @@ def cpu_baseline(method, seed, length, offsets_host, got, budget_s, samples, seg
             break
     med = float(np.median(laps))
     base = {"value": round(sample_bytes / med / 2**30, 2), "unit": "GiB/s", "cores": threads, "kind": "port",
-            "variant": "x86 SSE4.2 crc32 instruction" if variant == "sse42" else "slicing table",
+            "variant": "x86 SSE4.2 crc32 instruction" if variant == "sse42" else "slicing-by-8 tables",
             "sample": f"median of {len(laps)} passes over {what} of the same splitmix payloads "
                       f"({el:.2f} s wall, {threads} threads)"}
     base["cpus_visible"] = f"{affinity} in the affinity mask" + (f", cgroup quota {quota[0]:g} CPUs" if quota else "")
     # the other CPU paths on the same sample: 1 thread, and the
     # table path next to SSE4.2 for CRC-32C
-    legs = [("sse42" if variant == "sse42" else "table", 1)] + ([("table", threads)] if variant == "sse42" else [])
+    legs = [(variant, 1), ("table", threads)]  # 1 thread; the byte-table (Sarwate) path at full width
     breakdown = {}
     for v, th in legs:
         p2, t2 = 0, time.perf_counter()

@@ -61,6 +61,8 @@ uint64_t oracle_reg_final(const oracle_model_t *m, uint64_t reg);
 /* Byte-at-a-time table form (Sarwate), derived from the bitwise model at
  * run time; checked against it in tests.  Used for large fixtures. */
 uint64_t oracle_crc_table(const oracle_model_t *m, const void *data, size_t n);
+/* slicing-by-8 (reflected models; others fall back to the byte table) */
+uint64_t oracle_crc_slice8(const oracle_model_t *m, const void *data, size_t n);
 
 /* Independent hardware oracle: x86 SSE4.2 crc32 instruction (CRC-32C).
  * Returns 0 and sets *ok = 0 when the CPU lacks SSE4.2. */

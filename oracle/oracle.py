@@ -16,7 +16,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_build", "liboracle.so")
 
-VARIANT_TABLE, VARIANT_SSE42, VARIANT_BITWISE = 0, 1, 2
+VARIANT_TABLE, VARIANT_SSE42, VARIANT_BITWISE, VARIANT_SLICE8 = 0, 1, 2, 3
 
 
 class Model(ctypes.Structure):
@@ -53,6 +53,8 @@ def lib():
         L.oracle_crc_bitwise.argtypes = [P, ctypes.c_void_p, ctypes.c_size_t]
         L.oracle_crc_table.restype = ctypes.c_uint64
         L.oracle_crc_table.argtypes = [P, ctypes.c_void_p, ctypes.c_size_t]
+        L.oracle_crc_slice8.restype = ctypes.c_uint64
+        L.oracle_crc_slice8.argtypes = [P, ctypes.c_void_p, ctypes.c_size_t]
         L.oracle_crc32c_sse42.restype = ctypes.c_uint32
         L.oracle_crc32c_sse42.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int)]
         L.oracle_fill_splitmix.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64]
@@ -102,6 +104,8 @@ def crc(method: str, data, variant: str = "table") -> int:
     m = model(method)
     if variant == "bitwise":
         return int(lib().oracle_crc_bitwise(m, p, a.size))
+    if variant == "slice8":
+        return int(lib().oracle_crc_slice8(m, p, a.size))
     if variant == "sse42":
         ok = ctypes.c_int(0)
         v = lib().oracle_crc32c_sse42(p, a.size, ctypes.byref(ok))
@@ -128,7 +132,7 @@ def varlen_offsets(seed: int, count: int, min_len: int = 64, max_len: int = 6553
     return off
 
 
-_VAR = {"table": VARIANT_TABLE, "sse42": VARIANT_SSE42, "bitwise": VARIANT_BITWISE}
+_VAR = {"table": VARIANT_TABLE, "sse42": VARIANT_SSE42, "bitwise": VARIANT_BITWISE, "slice8": VARIANT_SLICE8}
 
 
 def batch_fixed(method, data: np.ndarray, stride: int, length: int, count: int, variant="table", nthreads=1):

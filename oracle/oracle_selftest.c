@@ -60,6 +60,11 @@ main(void)
             CHECK(oracle_crc_table(m, buf + (n % 13), n) ==
                       oracle_crc_bitwise(m, buf + (n % 13), n),
                 "%s table!=bitwise n=%zu", m->name, n);
+    for (m = oracle_models(); m->name; m++)
+        for (n = 0; n < 300; n += 5)
+            CHECK(oracle_crc_slice8(m, buf + (n % 11), n) ==
+                      oracle_crc_bitwise(m, buf + (n % 11), n),
+                "%s slice8!=bitwise n=%zu", m->name, n);
 
     oracle_crc32c_sse42("", 0, &ok);
     if (ok) {

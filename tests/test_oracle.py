@@ -108,3 +108,18 @@ def test_batch_helpers_agree(oracle_mod):
     off = np.arange(0, 300 * 1000 + 1, 1000, dtype=np.uint64)
     d = oracle_mod.batch_offsets("crc32c", buf, off, nthreads=5)
     assert np.array_equal(d, oracle_mod.batch_fixed("crc32c", buf, 1000, 1000, 300))
+
+
+def test_slice8_equals_bitwise_for_every_reflected_model(oracle_mod):
+    """The CPU baseline's slicing-by-8 path (bench.py cpu_baseline for crc64)
+    equals the literal bitwise model, at every length 0..70 and unaligned starts."""
+    import numpy as np
+    buf = oracle_mod.splitmix_bytes(4096, 0x51CE)
+    for m in ("crc32c", "crc32", "crc64", "crc64-xz", "crc64-jones", "crc64-go-iso", "crc16-arc", "crc16-kermit"):
+        for n in list(range(0, 71)) + [1000, 4093]:
+            for off in (0, 3):
+                d = buf[off:off + n]
+                assert oracle_mod.crc(m, d, variant="slice8") == oracle_mod.crc(m, d, variant="bitwise"), (m, n, off)
+    big = oracle_mod.splitmix_bytes(1 << 20, 3)
+    assert oracle_mod.batch_fixed("crc64", big, 1 << 18, 1 << 18, 4, variant="slice8").tolist() == \
+        oracle_mod.batch_fixed("crc64", big, 1 << 18, 1 << 18, 4, variant="table").tolist()

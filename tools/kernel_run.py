@@ -13,7 +13,23 @@ ap.add_argument("--config", default="c3")
 ap.add_argument("--iters", type=int, default=5)
 a = ap.parse_args()
 method, count, length, seed = SHAPES[a.config]
-if length is None:
+if a.config == "msgs":  # bench.py's msgs layout: HG header (network-order payload CRC) at 16, payload from 20
+    from mercury_amd.workload import varlen_offsets
+    off = varlen_offsets(seed, count)
+    data = torch.empty(int(off[-1]) + 64, dtype=torch.uint8, device="cuda")
+    G.fill_splitmix(data, seed)
+    inter = np.empty(2 * count + 1, dtype=np.uint64)
+    inter[0::2] = off
+    inter[1::2] = off[:-1] + np.uint64(20)
+    sender = G.checksum_offsets(method, data, torch.from_numpy(inter.astype(np.int64)).cuda())
+    offs = torch.from_numpy(off.astype(np.int64)).cuda()
+    crc = sender[1::2].to(torch.int64) & 0xFFFFFFFF
+    for k in range(4):
+        data[offs[:-1] + 16 + k] = ((crc >> (24 - 8 * k)) & 0xFF).to(torch.uint8)
+    status = torch.empty(count, dtype=torch.uint8, device="cuda")
+    mism = torch.zeros(1, dtype=torch.int32, device="cuda")
+    run = lambda: G.verify_messages(data, offs, status=status, mismatches=mism)
+elif length is None:
     from mercury_amd.workload import varlen_offsets
     off = varlen_offsets(seed, count)
     data = torch.empty(int(off[-1]) + 64, dtype=torch.uint8, device="cuda")

@@ -5,9 +5,10 @@
 in KiB; FETCH_SIZE reads exactly half the bytes of a wide coalesced streaming
 read on gfx950, so it is doubled.
 
-usage: pmc_traffic.py FETCH_DIR WRITE_DIR KERNEL_SUBSTRING OUT_JSON [alg_bytes [dispatches_per_call]]
+usage: pmc_traffic.py FETCH_DIR WRITE_DIR KERNEL_SUBSTRING OUT_JSON [alg_bytes [dispatches_per_call [last]]]
 (dispatches_per_call: kernels matching the substring per API call, e.g. 3 for
-the segments path: scan + two chunk passes)
+the segments path: scan + two chunk passes; last: use only the last N matching
+dispatches -- the timed calls, not a config's setup launches)
 """
 import csv
 import glob
@@ -23,15 +24,18 @@ def read(d, counter, ksub):
                 continue
             key = row.get("Dispatch_Id") or row.get("Correlation_Id")
             vals[key] = vals.get(key, 0.0) + float(row["Counter_Value"])
-    return list(vals.values())
+    return [vals[k] for k in sorted(vals, key=lambda k: int(k) if str(k).isdigit() else str(k))]
 
 
 def main():
     fdir, wdir, ksub, out = sys.argv[1:5]
     alg = float(sys.argv[5]) if len(sys.argv) > 5 else None
     per_call = int(sys.argv[6]) if len(sys.argv) > 6 else 1
+    last = int(sys.argv[7]) if len(sys.argv) > 7 else 0
     f = read(fdir, "FETCH_SIZE", ksub)
     w = read(wdir, "WRITE_SIZE", ksub)
+    if last:
+        f, w = f[-last:], w[-last:]
     if not f or not w:
         raise SystemExit(f"no counter rows for {ksub!r}: fetch={len(f)} write={len(w)}")
     fetch_b = 2 * 1024 * sum(f) / len(f) * per_call
