@@ -1241,6 +1241,22 @@ MCK_SDWA_P6(1)
 MCK_SDWA_P6(2)
 MCK_SDWA_P6(3)
 #undef MCK_SDWA_P6
+// bits 0..2 of each byte of x and bits 0..4 of each byte of (x >> 5): one
+// v_bfi_b32 (mask in an SGPR; VOP3 takes no literal on gfx9).  The C form
+// (x & m) | (y & ~m) compiled to v_and + v_and_or: one VALU op more per
+// 32-bit half on a VALU-bound loop.
+#ifndef MCK_BFI64
+#define MCK_BFI64 1
+#endif
+__device__ __forceinline__ uint32_t gather6(uint32_t x) {
+#if MCK_BFI64
+    uint32_t r;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(0x07070707u), "v"(x), "v"(x >> 5));
+    return r;
+#else
+    return (x & 0x07070707u) | ((x >> 5) & ~0x07070707u);
+#endif
+}
 __device__ __forceinline__ uint64_t xor13(const uint64_t *r, uint64_t extra) {
     const uint64_t a = xor3_64(r[0], r[1], r[2]), b = xor3_64(r[3], r[4], r[5]), c = xor3_64(r[6], r[7], r[8]);
     return xor3_64(a, b, xor3_64(c, xor3_64(r[9], r[10], r[11]), extra));
@@ -1249,8 +1265,8 @@ __device__ __forceinline__ uint64_t xor13(const uint64_t *r, uint64_t extra) {
 __device__ __forceinline__ uint64_t f64x(const uint8_t *lds, uint64_t x, uint64_t next, Lane64 &ln) {
     const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
     // byte 2i' of t: bits 0..2 of bytes 2i', 2i'+1 of the half (bit-select)
-    const uint32_t tl = (xl & 0x07070707u) | ((xl >> 5) & ~0x07070707u);
-    const uint32_t th = (xh & 0x07070707u) | ((xh >> 5) & ~0x07070707u);
+    const uint32_t tl = gather6(xl);
+    const uint32_t th = gather6(xh);
     uint64_t r[12];
     r[0] = lds64(lds, sdwa_f8_0(xl) + kL64P5 + 0 * 256);
     r[1] = lds64(lds, sdwa_f8_1(xl) + kL64P5 + 1 * 256);
