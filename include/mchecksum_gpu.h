@@ -26,12 +26,12 @@
  * Streams: `stream` is a hipStream_t (NULL = the default stream).  Calls are
  * asynchronous and capture-safe once mchecksum_gpu_prepare() has run for the
  * method on the current device (it uploads the lookup tables).  Large batches
- * balance their payloads through a device-side work-queue slot: eager calls
- * cycle through 3072 slots per device, captured calls through 1024 (a captured
- * call keeps its slot for every replay).  Slots are claimed by the running
- * launch, so launches that meet on one slot (more than 3072 calls in flight,
- * or two graph execs of one capture replayed at the same time) still hash
- * every payload: the later one takes a static split of the batch instead.
+ * balance their payloads through a device-side work-queue slot of their
+ * stream's own (up to 2048 streams per device; launches on one stream never
+ * overlap).  Calls captured into a hipGraph, calls on hipStreamPerThread and
+ * streams past the 2048th take a static split of the batch instead: a graph
+ * replays its captured arguments, possibly on two execs at once, so no slot
+ * could be exclusive to it.
  *
  * Fail closed: every wait in the work queue is bounded.  A launch in which a
  * wait gives up (a protocol fault; 0 in every test run) adds 1 to the error
@@ -64,8 +64,11 @@ extern "C" {
 MCHECKSUM_PUBLIC int
 mchecksum_gpu_available(void);
 
-/* Build and upload the lookup tables for hash_method on the current device.
- * Optional (done lazily on first use); call it before hipGraph capture. */
+/* Build and upload the lookup tables for hash_method on the current device:
+ * the payload kernels' packs and the Z^n shift pack (32/64-bit models), or
+ * the core-header byte table (16-bit models).  Optional (done lazily on first
+ * use); call it before hipGraph capture -- a first use inside a capture
+ * would upload tables there and invalidate the capture. */
 MCHECKSUM_PUBLIC int
 mchecksum_gpu_prepare(const char *hash_method);
 

@@ -154,11 +154,9 @@ struct BatchArgs {
     // message mode (verify_messages): payload i = [offsets[i] + pay_off,
     // offsets[i+1]), expected CRC = big-endian u32 at offsets[i] + hash_off
     uint32_t msg, pay_off, hash_off;
-    // work-queue slot (WgQueue below); nullptr = static assignment
+    // work-queue slot (WgQueue below), exclusive to this launch's stream;
+    // nullptr = static assignment
     unsigned long long *queue;
-    // 1: claim the slot's owner word (slots the host cannot hand out
-    // exclusively: graph-captured launches and overflow streams)
-    uint32_t own;
     // optional caller word (mchecksum_gpu_set_error_word): +1 when this launch
     // could not hash every payload (fail-closed report for checksum modes)
     uint32_t *err_word;
@@ -191,36 +189,31 @@ constexpr uint64_t kSplitBytes = 256u << 10;
 // readers of the previous occupant have read it.  Exit counting is
 // hierarchical (LDS per workgroup, one line per group, one per slot) and the
 // last group zeroes the slot for the next launch (the host hands each launch
-// a slot from a ring, mchecksum_gpu.hip).  tests/test_queue_model.py runs the
-// same protocol on the CPU under random interleavings.
+// a slot of its stream's own, mchecksum_gpu.hip).  tests/test_queue_model.py
+// runs the same protocol on the CPU under random interleavings.
 // Slot layout (one counter per 256-B line): [0, 8) sub-queue tickets,
 // [8, 16) exited workgroups per group (blockIdx % 8), [16] exited groups,
-// [17] fault flag of the launch, [18] owner tag.
+// [17] fault flag of the launch.
 //
-// Ownership.  A slot must only ever be used by one launch at a time.  The
-// host gives every stream a slot of its own (launches on one stream never
-// overlap), so eager launches need no check.  Where the host cannot promise
-// exclusivity -- a graph-captured launch keeps its slot for every replay, and
-// two graph execs of one capture may replay at the same time; streams beyond
-// the per-stream table share hashed slots -- the launch runs with own = 1:
-// every workgroup's first thread reads the owner word and, while it is 0,
-// claims it with a CAS of the launch's tag (its kernarg address -- distinct
-// for any two launches that run at the same time); the last group releases
-// it, owner word last.  (Same-address reads and CASes from 256 workgroups
-// serialise at one L2 channel: ~0.5% of the headline launch, so eager
-// launches skip it.)  A workgroup that finds the slot owned by another launch
-// never touches it and takes the static split instead (units wave,
-// wave + #waves, ...): every unit is still hashed, at the static split's speed.  (If some workgroups of one launch see the slot busy and
-// later ones see it free, the static ones repeat units the queue also hands
-// out: CRCs are written twice with the same value; verify mismatch counts may
-// then over-count, never under-count.)
+// Exclusivity.  A slot serves one launch at a time: the host hands the queue
+// only to eager launches, each on a slot of its stream's own (launches on one
+// stream never overlap).  Launches it cannot give an exclusive slot -- graph
+// captures (every replay reuses the captured arguments, and two execs of one
+// capture may replay at once) and streams past the per-stream table -- get
+// no slot and take the static split (units wave, wave + #waves, ...).  (Round
+// 2 had such launches claim a shared slot with a tag; a launch whose early
+// workgroups found the slot busy and later ones found it free never released
+// it, and its next replay -- same tag -- ran on stale counters and skipped
+// units: one wrong batch in 400 concurrent replays.  The XOR-accumulating
+// kernels (split CRC-64 pieces, scatter-gather chunks) also cannot tolerate
+// the units such mixed launches hashed twice.)
 constexpr uint32_t kQSub = 8;
 constexpr uint32_t kQStride = 32;  // u64 words between counters
 constexpr uint32_t kQGroupDone = kQSub;
 constexpr uint32_t kQAllDone = 2 * kQSub;
 constexpr uint32_t kQFault = 2 * kQSub + 1;
-constexpr uint32_t kQOwner = 2 * kQSub + 2;
-constexpr uint32_t kQSlotWords = (2 * kQSub + 3) * kQStride;
+constexpr uint32_t kQSlotLines = 2 * kQSub + 2;
+constexpr uint32_t kQSlotWords = kQSlotLines * kQStride;
 // Chunk size: a power of two, about a quarter of a workgroup's fair share
 // of units, between 1 and 32 (C4: 32 units; a 5000-payload batch: 4).
 // Fixed 16 starved half the workgroups of C3's 8192 units at 2 WGs per CU; 32
@@ -285,7 +278,7 @@ struct WgQueue {
     unsigned int slot;     // next (chunk, unit) slot of this workgroup
     unsigned int drained;  // sub-queues (counted from home) found empty
     unsigned int exited;   // waves of this workgroup that left the loop
-    unsigned int busy;     // 1: the slot belongs to another launch -> static split
+    unsigned int busy;     // 1: no slot for this launch -> static split
     unsigned int reads[kWgRing];
     unsigned long long entry[kWgRing];  // (chunk seq << 32) | global chunk id
 };
@@ -384,44 +377,26 @@ __device__ bool wg_publish(WgQueue *L, uint32_t seq, uint64_t id, uint32_t cl) {
     return ok;
 }
 
-// The launch's tag: its kernarg segment address.  Two launches that run at
-// the same time never share one (each reads its own arguments while it runs).
-__device__ __forceinline__ unsigned long long launch_tag() {
-    return reinterpret_cast<uint64_t>(__builtin_amdgcn_kernarg_segment_ptr());
-}
-
-// Thread 0, before the kernel's first barrier: reset the LDS state, claim the
-// slot for this launch when the host asks for it (own: see "Ownership") and
-// publish the first chunk (its fetch overlaps the LDS table fill).  A slot
-// owned by another launch is left alone: the workgroup then takes the static
-// split (busy = 1).
-__device__ __attribute__((unused)) void wg_queue_init(WgQueue *L, unsigned long long *q, uint64_t n, bool own) {
+// Thread 0, before the kernel's first barrier: reset the LDS state and
+// publish the first chunk (its fetch overlaps the LDS table fill).  Without a
+// slot (see "Exclusivity") the workgroup takes the static split (busy = 1).
+__device__ __attribute__((unused)) void wg_queue_init(WgQueue *L, unsigned long long *q, uint64_t n) {
     L->slot = 0;
     L->drained = 0;
     L->exited = 0;
-    L->busy = 0;
+    L->busy = q == nullptr;
     for (uint32_t r = 0; r < kWgRing; r++) {
         L->reads[r] = 0;
         L->entry[r] = ~0ull;
     }
-    if (own) {
-        unsigned long long *ow = q + kQOwner * kQStride;
-        const unsigned long long tag = launch_tag();
-        unsigned long long owner = __hip_atomic_load(ow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (owner == 0ull) owner = atomicCAS(ow, 0ull, tag);
-        if (owner != 0ull && owner != tag) {
-            L->busy = 1;
-            return;
-        }
-    }
+    if (!q) return;
     const ChunkPlan plan(n);
     (void)wg_publish(L, 0, wg_fetch(L, q, plan.nch), plan.cl);
 }
 
 // Calls body(u) for this wave's units: through the work queue (DYN: the
-// throughput kernels; the host always passes a slot, wg_queue_init has run)
-// or u = wave, wave + nw, ... (the light layout's small batches, and a DYN
-// workgroup whose slot belongs to another launch).
+// throughput kernels, wg_queue_init has run) or u = wave, wave + nw, ... (the
+// light layout's small batches, and DYN launches without a slot).
 //
 // Fail closed.  Every wait of the queue protocol is bounded; a wave whose wait
 // gives up leaves the loop, and the units it would still have taken may then
@@ -434,7 +409,7 @@ __device__ __attribute__((unused)) void wg_queue_init(WgQueue *L, unsigned long 
 #endif
 template <bool DYN, class F>
 __device__ __forceinline__ bool for_each_unit(WgQueue *L, unsigned long long *queue, uint64_t n, uint32_t wave,
-                                              uint32_t nw, bool own, F &&body) {
+                                              uint32_t nw, F &&body) {
     if constexpr (DYN) {
         // One call site of body for both splits: a second inlined copy of the
         // payload loop made the offsets kernels spill, and so does the copy
@@ -545,7 +520,7 @@ __device__ __forceinline__ bool for_each_unit(WgQueue *L, unsigned long long *qu
             g_mck_qwave[4 * 16384 + 2 * wave + 1] = qs_busy;
         }
 #endif
-        if (__builtin_amdgcn_readfirstlane(lds_ld(&L->busy))) return false;  // never touched the slot
+        if (__builtin_amdgcn_readfirstlane(lds_ld(&L->busy))) return false;  // no slot
         // The first faulting wave of the launch claims the slot's fault flag
         // (before its own exit is counted, so the slot cannot be released yet).
         uint32_t first = 0;
@@ -554,8 +529,8 @@ __device__ __forceinline__ bool for_each_unit(WgQueue *L, unsigned long long *qu
         // single line serialised ~4096 x 45 ns at the end of every launch
         // (C2 ran 2x slower).  Waves count in LDS, the last wave of a
         // workgroup counts in its group's line, the last workgroup of a group
-        // in the slot's line; the last group zeroes the slot and releases it,
-        // the owner word last (after every other zero has reached L2).
+        // in the slot's line; the last group zeroes the slot for the next
+        // launch on this stream.
         uint32_t last = 0;
         if (l0 && atomicAdd(&L->exited, 1u) == blockDim.x / 64u - 1u) {
             const uint32_t g = blockIdx.x % kQSub;
@@ -566,16 +541,11 @@ __device__ __forceinline__ bool for_each_unit(WgQueue *L, unsigned long long *qu
         }
         if (__builtin_amdgcn_readfirstlane(last)) {  // one instruction: lane j zeroes line j
             const uint32_t j = threadIdx.x & 63u;
-            if (j < kQOwner) atomicExch(queue + j * kQStride, 0ull);
-            if (own) {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                if (j == 0) atomicExch(queue + kQOwner * kQStride, 0ull);
-            }
+            if (j < kQSlotLines) atomicExch(queue + j * kQStride, 0ull);
         }
         (void)nw;
         return __builtin_amdgcn_readfirstlane(first) != 0;
     } else {
-        (void)own;
         for (uint64_t u = wave; u < n; u += nw) body(u);
         return false;
     }
@@ -1047,7 +1017,7 @@ __global__ __launch_bounds__(kBlk32<LIGHT>, 1) void crc32c_batch_kernel(BatchArg
 #if defined(MCK_EMPTY) && MCK_EMPTY == 2
     if (!DYN) return;  // diagnostic: launch cost alone
 #endif
-    if (DYN && threadIdx.x == 0) wg_queue_init(&wgq, a.queue, units, a.own);
+    if (DYN && threadIdx.x == 0) wg_queue_init(&wgq, a.queue, units);
     fill_lds32<LIGHT, kBlk32<LIGHT>>(lds_raw, pk);
     __syncthreads();
 #if defined(MCK_EMPTY) && MCK_EMPTY == 1
@@ -1083,7 +1053,7 @@ __global__ __launch_bounds__(kBlk32<LIGHT>, 1) void crc32c_batch_kernel(BatchArg
             }
         };
         if constexpr (!LIGHT) {
-            if (for_each_unit<true>(&wgq, a.queue, units, wave, nw, a.own, one)) fail_closed<VERIFY>(a);
+            if (for_each_unit<true>(&wgq, a.queue, units, wave, nw, one)) fail_closed<VERIFY>(a);
         } else {  // static: a byte-balanced contiguous range per wave
             uint64_t first, last;
             wave_range(a.offsets, a.count, wave, nw, &first, &last);
@@ -1092,7 +1062,7 @@ __global__ __launch_bounds__(kBlk32<LIGHT>, 1) void crc32c_batch_kernel(BatchArg
         MCK_STAMP(wave, 2);
         return;
     }
-    const bool faulted = for_each_unit<DYN>(&wgq, a.queue, units, wave, nw, a.own, [&](uint64_t u) {
+    const bool faulted = for_each_unit<DYN>(&wgq, a.queue, units, wave, nw, [&](uint64_t u) {
         const uint64_t p = u * PPW + grp;
         const bool act = p < a.count;
         const uint64_t pc = act ? p : a.count - 1;
@@ -1559,7 +1529,7 @@ __global__ __launch_bounds__(kBlk64<MODE>, kWpe64<MODE>) void crc64_batch_kernel
     __shared__ WgQueue wgq;
     constexpr bool DYN = dyn_policy(64, MODE, NT, false) || SPLIT;
     MCK_STAMP(blockIdx.x * kWPB + (threadIdx.x >> 6), 0);
-    if (DYN && threadIdx.x == 0) wg_queue_init(&wgq, a.queue, units, a.own);
+    if (DYN && threadIdx.x == 0) wg_queue_init(&wgq, a.queue, units);
     fill_lds64<S::block, S::ops_mode>(lds, pk);
     __syncthreads();
     MCK_STAMP(blockIdx.x * kWPB + (threadIdx.x >> 6), 1);
@@ -1585,14 +1555,14 @@ __global__ __launch_bounds__(kBlk64<MODE>, kWpe64<MODE>) void crc64_batch_kernel
                                                 : payload64_generic<LOG2G, NT, S::ops_mode>(lds, pk, a.base + o, n, gl, lc);
             if (gl == 0) emit<uint64_t, VERIFY>(a, p, x ^ xorout);
         };
-        if (for_each_unit<true>(&wgq, a.queue, units, wave, nw, a.own, one)) fail_closed<VERIFY>(a);
+        if (for_each_unit<true>(&wgq, a.queue, units, wave, nw, one)) fail_closed<VERIFY>(a);
         return;
     }
     if constexpr (SPLIT) {
         static_assert(LOG2G == 6 && MODE == kFixedAligned && !VERIFY, "split pieces: aligned G = 64 checksums");
         const uint32_t sl = a.split_log2, pieces = 1u << sl;
         const crc64_shift_pack_t *sp = reinterpret_cast<const crc64_shift_pack_t *>(a.shift);
-        const bool faulted = for_each_unit<true>(&wgq, a.queue, units, wave, nw, a.own, [&](uint64_t u) {
+        const bool faulted = for_each_unit<true>(&wgq, a.queue, units, wave, nw, [&](uint64_t u) {
             const uint64_t p = u >> sl;
             const uint32_t q = (uint32_t)u & (pieces - 1);
             const uint64_t x = payload64_aligned<6, NT, S::ops_global>(
@@ -1606,7 +1576,7 @@ __global__ __launch_bounds__(kBlk64<MODE>, kWpe64<MODE>) void crc64_batch_kernel
         if (faulted) fail_closed<false>(a);
         return;
     }
-    const bool faulted = for_each_unit<DYN>(&wgq, a.queue, units, wave, nw, a.own, [&](uint64_t u) {
+    const bool faulted = for_each_unit<DYN>(&wgq, a.queue, units, wave, nw, [&](uint64_t u) {
         const uint64_t p = u * PPW + grp;
         const bool act = p < a.count;
         const uint64_t pc = act ? p : a.count - 1;

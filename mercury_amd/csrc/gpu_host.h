@@ -25,21 +25,14 @@ struct DevCtx {
     // Work-queue slots of the batch kernels (WgQueue, crc_gpu_device.h):
     // kQueueSlots zeroed counter sets; a launch's last group re-zeroes its slot.
     // Eager launches use a slot of their stream's own (the first kStreamSlots
-    // streams seen on the device; launches on one stream never overlap).  A
-    // launch captured into a hipGraph keeps its slot for every replay: those
-    // come round-robin from kCapturedSlots; streams past the table share
-    // kOverflowSlots by hash.  Both of those claim the slot on the device
-    // (BatchArgs::own) and a launch that finds it owned by another running
-    // launch takes the static split (crc_gpu_device.h, "Ownership"), so a
-    // collision costs speed, never correctness.
+    // streams seen on the device; launches on one stream never overlap).
+    // Graph-captured launches and streams past the table get none and take
+    // the static split (crc_gpu_device.h, "Exclusivity").
     unsigned long long *queue = nullptr;
-    uint32_t queue_captured = 0;
     std::unordered_map<void *, uint32_t> stream_slot;  // guarded by g_mu
 };
 constexpr uint32_t kStreamSlots = 2048;
-constexpr uint32_t kCapturedSlots = 1024;
-constexpr uint32_t kOverflowSlots = 1024;
-constexpr uint32_t kQueueSlots = kStreamSlots + kCapturedSlots + kOverflowSlots;
+constexpr uint32_t kQueueSlots = kStreamSlots;
 
 extern std::mutex g_mu;
 
@@ -57,8 +50,11 @@ int prologue(const char *method, int log2g, int *width, DevCtx **c, const void *
 // (caller holds g_mu).
 int get_ext(DevCtx *c, int idx, const void **out);
 // Work-queue slot for one launch of a throughput (non-light) batch kernel on
-// `stream`; *own = 1 when the launch must claim it on the device.
-unsigned long long *queue_slot(DevCtx *c, void *stream, uint32_t *own);
+// `stream`, exclusive to that stream; nullptr (static split) for a launch
+// being captured into a graph or a stream past the table.
+unsigned long long *queue_slot(DevCtx *c, void *stream);
+// This host thread's fail-closed report word (mchecksum_gpu_set_error_word), or nullptr.
+uint32_t *error_word();
 
 }  // namespace mck
 

@@ -144,42 +144,34 @@ int get_pack(DevCtx *c, int idx, int log2g, const void **pack) {
     return 0;
 }
 
-unsigned long long *queue_slot(DevCtx *c, void *stream, uint32_t *own) {
+unsigned long long *queue_slot(DevCtx *c, void *stream) {
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing((hipStream_t)stream, &st) != hipSuccess) {
         (void)hipGetLastError();
         st = hipStreamCaptureStatusNone;
     }
-    if (st == hipStreamCaptureStatusActive) {
-        // Captured launches keep their slot for every replay, round-robin over
-        // the captured range; the kernel claims it (two replays that meet on
-        // one slot stay correct: the later one takes the static split).
-        // (MCHECKSUM_GPU_CAPTURED_SLOTS=n, tests only: use n captured slots)
-        static const uint32_t ncap = [] {
-            const char *e = getenv("MCHECKSUM_GPU_CAPTURED_SLOTS");
-            const long v = e && e[0] ? atol(e) : 0;
-            return v >= 1 && v <= (long)kCapturedSlots ? (uint32_t)v : kCapturedSlots;
-        }();
-        const uint32_t k = __atomic_fetch_add(&c->queue_captured, 1u, __ATOMIC_RELAXED) % ncap;
-        *own = 1;
-        return c->queue + (size_t)(kStreamSlots + k) * kQSlotWords;
-    }
-    {
-        std::lock_guard<std::mutex> lk(g_mu);
-        auto it = c->stream_slot.find(stream);
-        if (it == c->stream_slot.end() && c->stream_slot.size() < kStreamSlots)
-            it = c->stream_slot.emplace(stream, (uint32_t)c->stream_slot.size()).first;
-        if (it != c->stream_slot.end()) {
-            *own = 0;  // this stream's own slot: its launches never overlap
-            return c->queue + (size_t)it->second * kQSlotWords;
-        }
-    }
-    const uint64_t h = ((uint64_t)(uintptr_t)stream >> 4) * 0x9E3779B97F4A7C15ull;
-    *own = 1;
-    return c->queue + (size_t)(kStreamSlots + kCapturedSlots + (uint32_t)((h >> 32) % kOverflowSlots)) * kQSlotWords;
+    // A captured launch replays with these arguments, possibly on two graph
+    // execs at once: no exclusive slot exists for it, so it takes the static
+    // split (crc_gpu_device.h, "Exclusivity").
+    if (st != hipStreamCaptureStatusNone) return nullptr;
+    // hipStreamPerThread names a different stream in every host thread: one
+    // slot for that handle could serve two launches at once
+    if ((hipStream_t)stream == hipStreamPerThread) return nullptr;
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = c->stream_slot.find(stream);
+    if (it == c->stream_slot.end() && c->stream_slot.size() < kStreamSlots)
+        it = c->stream_slot.emplace(stream, (uint32_t)c->stream_slot.size()).first;
+    // this stream's own slot (its launches never overlap), or none past the table
+    return it != c->stream_slot.end() ? c->queue + (size_t)it->second * kQSlotWords : nullptr;
 }
 
+uint32_t *error_word() { return t_err_word; }
+
 typedef void (*kern_t)(BatchArgs);
+
+__global__ __launch_bounds__(256) void zero_u64_kernel(unsigned long long *p, uint64_t n) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) p[i] = 0;
+}
 
 struct KLaunch {
     kern_t k;
@@ -335,7 +327,7 @@ int do_offsets(const char *method, const void *base, const uint64_t *offsets, si
     else
         k = verify ? (nt ? kernel_ptr<64, 6, kOffsets, true, true>() : kernel_ptr<64, 6, kOffsets, true>())
                    : (nt ? kernel_ptr<64, 6, kOffsets, false, true>() : kernel_ptr<64, 6, kOffsets, false>());
-    if (dyn_policy(width, kOffsets, nt, light)) a.queue = queue_slot(c, stream, &a.own);
+    if (dyn_policy(width, kOffsets, nt, light)) a.queue = queue_slot(c, stream);
     return launch(k, a, grid_for(c, count, k), stream);
 }
 
@@ -382,9 +374,16 @@ int launch_fixed(DevCtx *c, int idx, const void *pack, int width, int lg, const 
         }
         a.shift = shift;
         a.split_log2 = sl;
-        a.queue = queue_slot(c, stream, &a.own);
-        // the pieces XOR their terms into out[]: zero it first (in stream order)
-        hipError_t e = hipMemsetAsync(dev_out, 0, count * sizeof(uint64_t), (hipStream_t)stream);
+        a.queue = queue_slot(c, stream);
+        // the pieces XOR their terms into out[]: zero it first, in stream order,
+        // with a kernel -- a hipMemsetAsync captured into a graph did not order
+        // against the kernel node on replays after the first (the pieces landed
+        // in a half-zeroed output: tests/test_gpu_queue.py, concurrent replays)
+        uint64_t zb = (count + 255) / 256;
+        zb = zb > 1024 ? 1024 : zb;
+        hipLaunchKernelGGL(zero_u64_kernel, dim3((unsigned)zb), dim3(256), 0, (hipStream_t)stream,
+                           reinterpret_cast<unsigned long long *>(dev_out), (uint64_t)count);
+        hipError_t e = hipGetLastError();
         if (e != hipSuccess) return hip_err(e, "output zeroing");
         const KLaunch k = nt ? KLaunch{crc64_batch_kernel<6, kFixedAligned, false, true, true>, Shape<64, kFixedAligned>::block,
                                        Shape<64, kFixedAligned>::blocks_per_cu}
@@ -394,7 +393,7 @@ int launch_fixed(DevCtx *c, int idx, const void *pack, int width, int lg, const 
     }
     const KLaunch k = width == 32 ? pick_fixed<32>(lg, aligned, nt, light) : pick_fixed<64>(lg, aligned, nt, false);
     const uint64_t ppw = 64u >> lg;
-    if (dyn_policy(width, aligned ? kFixedAligned : kFixedGeneric, nt, light)) a.queue = queue_slot(c, stream, &a.own);
+    if (dyn_policy(width, aligned ? kFixedAligned : kFixedGeneric, nt, light)) a.queue = queue_slot(c, stream);
     const uint64_t units = (count + ppw - 1) / ppw;
     unsigned blocks = grid_for(c, units, k);
     // CRC-64 static split with fewer units than one full workgroup per CU:
@@ -430,14 +429,25 @@ int mchecksum_gpu_available(void) {
 
 int mchecksum_gpu_prepare(const char *hash_method) {
     if (!mchecksum_gpu_available()) return set_err(MCHECKSUM_GPU_ENODEV, "no HIP device");
-    for (int lg = 0; lg <= CRC_GPU_MAX_LOG2G; lg++) {
-        int width = 0;
-        DevCtx *c = nullptr;
-        const void *pack = nullptr;
-        int rc = prologue(hash_method, lg, &width, &c, &pack);
-        if (rc) return rc;
+    const int idx = mck_model_index(hash_method);
+    if (idx < 0) return set_err(MCHECKSUM_GPU_EMETHOD, "unknown hash method \"%s\"", hash_method ? hash_method : "(null)");
+    DevCtx *c = nullptr;
+    if (mck_models[idx].width != 16) {  // payload kernels: a table pack per lanes-per-payload width
+        for (int lg = 0; lg <= CRC_GPU_MAX_LOG2G; lg++) {
+            int width = 0;
+            const void *pack = nullptr;
+            int rc = prologue(hash_method, lg, &width, &c, &pack);
+            if (rc) return rc;
+        }
     }
-    return MCHECKSUM_GPU_OK;
+    // ... and the extension tables every entry point may need (Z^n shift pack:
+    // split CRC-64 pieces, segments, XDR; CRC-16 byte table: core headers),
+    // so that no call captured into a graph uploads anything
+    std::lock_guard<std::mutex> lk(g_mu);
+    int rc = device_ctx(&c);
+    if (rc) return rc;
+    const void *ext = nullptr;
+    return get_ext(c, idx, &ext);
 }
 
 int mchecksum_gpu_lanes_per_payload(const char *hash_method, size_t len) {

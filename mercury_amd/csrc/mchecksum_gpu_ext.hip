@@ -60,6 +60,10 @@ struct SegArgs {
     const unsigned long long *ragged;  // workspace: non-zero if any chunk needs the ragged loop
     void *out;
     const void *pack, *shift;
+    // work-queue slot of the chunk passes (crc_gpu_device.h, WgQueue; nullptr:
+    // static split) and the caller's fail-closed word
+    unsigned long long *queue;
+    uint32_t *err_word;
 };
 
 // Exclusive prefix sums of segment bytes (P) and chunk counts (C) in three
@@ -240,6 +244,68 @@ struct ChunkWalk {
     }
 };
 
+// Work-queue chunk passes (MCK_SEG_QUEUE=1, an A/B build): chunks are the
+// queue's units, so a wave holds chunks from anywhere in the list and finds
+// each one's segment and object by search.  The guess (chunk index scaled by
+// segments per chunk, segment index by objects per segment) is exact for
+// uniform segment and object sizes -- two scalar loads -- and a gallop +
+// binary search bounds the rest.  Measured against the static contiguous
+// ranges: `seg` (CRC-64) 1.515 vs 1.439 ms, CRC-32C 1.301 vs 1.295 ms
+// (profiles/r02/ab_seg_queue.log) -- so the default stays static.
+#ifndef MCK_SEG_QUEUE
+#define MCK_SEG_QUEUE 0
+#endif
+
+// The last i in [0, n) with A[i] <= key, for non-decreasing A with
+// A[0] <= key < A[n] (n >= 1), searched from the guess g.
+__device__ uint64_t seg_find(const uint64_t *A, uint64_t n, uint64_t key, uint64_t g) {
+    uint64_t lo, hi;  // A[lo] <= key < A[hi]
+    g = g < n ? g : n - 1;
+    if (A[g] <= key) {
+        lo = g;
+        hi = g + 1;
+        for (uint64_t step = 1; hi < n && A[hi] <= key; step <<= 1) {
+            lo = hi;
+            hi = n - lo > 2 * step ? lo + 2 * step : n;
+        }
+    } else {
+        hi = g;
+        lo = g - 1;  // g >= 1 here: A[0] <= key
+        for (uint64_t step = 1; lo > 0 && A[lo] > key; step <<= 1) {
+            hi = lo;
+            lo = lo > 2 * step ? lo - 2 * step : 0;
+        }
+    }
+    while (hi - lo > 1) {
+        const uint64_t mid = lo + (hi - lo) / 2;
+        if (A[mid] <= key) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__device__ __forceinline__ uint64_t seg_guess(uint64_t i, uint64_t n, uint64_t total) {
+    return total ? (uint64_t)((double)i * (double)n / (double)total) : 0;
+}
+
+// Chunk c (< C[nseg]): its bytes [addr, addr + n) and, when its segment
+// belongs to an object (*in), the object and the object bytes after it.
+// c is wave-uniform, so every load is scalar.
+__device__ __forceinline__ __attribute__((unused)) void seg_locate(const SegArgs &a, uint64_t c, uint64_t nchunks, uint64_t *addr, uint64_t *n,
+                                           bool *in, uint64_t *obj, uint64_t *after) {
+    const uint64_t s = seg_find(a.C, a.nseg, c, seg_guess(c, a.nseg, nchunks));
+    const uint64_t off = (c - a.C[s]) * kChunk, L = a.len[s];
+    *addr = a.addr[s] + off;
+    *n = L - off < kChunk ? L - off : kChunk;
+    const uint64_t f0 = a.first[0], f1 = a.first[a.nobj];
+    *in = s >= f0 && s < f1;
+    if (*in) {
+        const uint64_t j = seg_find(a.first, a.nobj, s, seg_guess(s - f0, a.nobj, f1 - f0));
+        *obj = j;
+        *after = a.P[a.first[j + 1]] - (a.P[s] + off + *n);
+    }
+}
+
 // Each object's Z^N(init) ^ xorout term (N = its byte count), XORed into
 // out[j] next to the chunk terms.  Latency-bound (up to 12 dependent table
 // applications per object), no LDS: the CRC-64 ragged pass runs only this when
@@ -282,7 +348,31 @@ __global__ __launch_bounds__(1024, kSegWavesPerEU<W * 4 + PART>) void seg_kernel
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWPB + (threadIdx.x >> 6));
     const uint32_t nw = gridDim.x * kWPB;
-    const uint64_t nchunks = a.C[a.nseg];
+    const uint64_t nchunks = uniform(a.C[a.nseg]);
+    // chunk passes with the work queue: PART 0 and PART 1 (the host passes a slot)
+    constexpr bool kQueue = MCK_SEG_QUEUE && PART != 2;
+    __shared__ WgQueue wgq;
+    if (kQueue && threadIdx.x == 0) wg_queue_init(&wgq, a.queue, nchunks);
+    // Calls body(addr, n, j, after) for every chunk of this wave that belongs
+    // to an object; true in the first wave of a launch whose queue wait gave
+    // up (the caller's error word then gets +1: fail closed).
+    auto chunks = [&](auto &&body) -> bool {
+        if constexpr (kQueue) {
+            return for_each_unit<true>(&wgq, a.queue, nchunks, wave, nw, [&](uint64_t c) {
+                uint64_t p, n, j = 0, after = 0;
+                bool in;
+                seg_locate(a, c, nchunks, &p, &n, &in, &j, &after);
+                if (in) body(p, n, j, after);
+            });
+        } else {
+            ChunkWalk walk(a, wave, nw, nchunks);
+            uint64_t p, n, j, after;
+            bool in;
+            while (walk.next(&p, &n, &in, &j, &after))
+                if (in) body(p, n, j, after);
+            return false;
+        }
+    };
     if constexpr (W == 32) {
         __shared__ __attribute__((aligned(16))) uint8_t lds_raw[kL32Bytes];
         const crc32_gpu_pack_t *pk = reinterpret_cast<const crc32_gpu_pack_t *>(a.pack);
@@ -293,11 +383,7 @@ __global__ __launch_bounds__(1024, kSegWavesPerEU<W * 4 + PART>) void seg_kernel
         const uint32_t lc0 = (lane & 31u) << 2, lc1 = lc0 | 0x10000u;
         uint32_t *out = reinterpret_cast<uint32_t *>(a.out);
         const bool nt = uniform(a.P[a.nseg]) >= kSegNtBytes;  // as for CRC-64 below
-        ChunkWalk walk(a, wave, nw, nchunks);
-        uint64_t p, n, j, after;
-        bool in;
-        while (walk.next(&p, &n, &in, &j, &after)) {
-            if (!in) continue;
+        const bool faulted = chunks([&](uint64_t p, uint64_t n, uint64_t j, uint64_t after) {
             const uint8_t *q = reinterpret_cast<const uint8_t *>(p);
             // whole rings of 1 KiB steps from a 16-B aligned start (the usual
             // bulk segment) take the aligned loop: no edge masks, no pad operator
@@ -307,7 +393,8 @@ __global__ __launch_bounds__(1024, kSegWavesPerEU<W * 4 + PART>) void seg_kernel
                                           : payload32_g64<false, Tab32<false>, true>(lds, pk, q, n, lane, lc0, lc1);
             x = shift32(sp, uniform(x), after);
             if (lane == 0) atomicXor(out + j, x);
-        }
+        });
+        if (faulted && lane == 0 && a.err_word) atomicAdd(a.err_word, 1u);
         seg_object_terms<32>(a);
     } else {
         // aligned chunks under the 12-lookup fold: combine operators from
@@ -326,14 +413,10 @@ __global__ __launch_bounds__(1024, kSegWavesPerEU<W * 4 + PART>) void seg_kernel
         // branch per chunk: +3% on `seg` (duplicating the whole walk under one
         // branch measured the same and spills more).
         [[maybe_unused]] const bool nt = uniform(a.P[a.nseg]) >= kSegNtBytes;
-        ChunkWalk walk(a, wave, nw, nchunks);
-        uint64_t p, n, j, after;
-        bool in;
-        while (walk.next(&p, &n, &in, &j, &after)) {
-            if (!in) continue;
+        const bool faulted = chunks([&](uint64_t p, uint64_t n, uint64_t j, uint64_t after) {
             const uint8_t *q = reinterpret_cast<const uint8_t *>(p);
             const bool aligned = p % 16 == 0 && n % 1024 == 0;
-            if (aligned != (PART == 1)) continue;
+            if (aligned != (PART == 1)) return;
             uint64_t x;
             if constexpr (PART == 1)
                 x = nt ? payload64_aligned<6, true, OG>(lds, pk, q, (uint32_t)(n >> 10), lane, lc, 0ull)
@@ -342,7 +425,8 @@ __global__ __launch_bounds__(1024, kSegWavesPerEU<W * 4 + PART>) void seg_kernel
                 x = payload64_g64<false, true>(lds, pk, q, n, lane, lc);
             x = shift64(sp, uniform(x), after);
             if (lane == 0) atomicXor(out + j, (unsigned long long)x);
-        }
+        });
+        if (faulted && lane == 0 && a.err_word) atomicAdd(a.err_word, 1u);
         if constexpr (PART == 1) return;
         seg_object_terms<64>(a);
     }
@@ -633,6 +717,8 @@ int mchecksum_gpu_checksum_segments(const char *hash_method, const uint64_t *dev
     a.out = dev_out;
     a.pack = pack;
     a.shift = shift;
+    a.err_word = error_word();
+    if (MCK_SEG_QUEUE) a.queue = queue_slot(c, stream);
     const uint64_t nb = (nseg + kScanBlk - 1) / kScanBlk;
     uint64_t *tot = (uint64_t *)dev_work + 2 * (nseg + 1) + 2;
     const uint64_t out_words = (uint64_t)nobj * (uint64_t)(width / 32);

@@ -83,9 +83,9 @@ def test_dynamic_queue_random_shapes(gpu, oracle_mod, n_iter, monkeypatch):
 
 
 def test_queue_slot_survives_graph_replay(gpu, oracle_mod, monkeypatch):
-    """A captured call keeps its work-queue slot; the last wave re-zeroes it, so
-    every replay distributes the whole batch again (offsets batch + an NT
-    fixed batch, both on the queue)."""
+    """Captured calls (an offsets batch and an NT fixed batch, both queue
+    kernels) replay with the static split -- no slot is baked into the graph
+    -- and every replay hashes the whole batch again."""
     import torch
     G, O = gpu, oracle_mod
     monkeypatch.setenv("MCHECKSUM_GPU_LIGHT", "0")
@@ -119,8 +119,8 @@ def test_queue_slot_survives_graph_replay(gpu, oracle_mod, monkeypatch):
 
 
 def test_concurrent_streams_get_distinct_slots(gpu, oracle_mod, monkeypatch):
-    """Queue-driven launches on four streams at once (each takes its own slot
-    from the ring) all return the oracle's values."""
+    """Queue-driven launches on four streams at once (each stream has a slot
+    of its own) all return the oracle's values."""
     import torch
     G, O = gpu, oracle_mod
     monkeypatch.setenv("MCHECKSUM_GPU_LIGHT", "0")
@@ -150,9 +150,9 @@ def test_concurrent_streams_get_distinct_slots(gpu, oracle_mod, monkeypatch):
 
 
 def test_graph_slot_is_never_reused_by_eager_launches(gpu, oracle_mod, monkeypatch):
-    """A captured launch owns its queue slot: 4300 eager launches on another
-    stream wrap the eager ring more than once while the graph keeps replaying
-    concurrently, and neither side loses or repeats a unit."""
+    """4300 eager queue launches on one stream while a captured launch of the
+    same kernel keeps replaying on another: the graph never touches the eager
+    stream's slot, and neither side loses or repeats a unit."""
     import torch
     G, O = gpu, oracle_mod
     monkeypatch.setenv("MCHECKSUM_GPU_LIGHT", "0")
@@ -192,53 +192,70 @@ def test_graph_slot_is_never_reused_by_eager_launches(gpu, oracle_mod, monkeypat
     assert bad == 0 and G.queue_faults() == 0
 
 
-def test_captured_launches_sharing_one_slot_stay_correct(gpu, oracle_mod):
-    """Two graphs captured onto ONE work-queue slot (MCHECKSUM_GPU_CAPTURED_SLOTS=1,
-    a test knob read once per process -- so this runs in a child process) and
-    replayed concurrently on two streams: the slot's owner word sends whichever
-    launch finds it taken to the static split, so both keep returning the
-    oracle's values (crc_gpu_device.h, "Ownership")."""
-    import subprocess
-    import sys
-    code = r"""
-import os, sys, numpy as np, torch
-sys.path.insert(0, os.environ["ROOT"])
-from mercury_amd import gpu as G
-from oracle import oracle as O
-host = O.splitmix_bytes(8 << 20, 31337)
-dev = torch.cat([torch.from_numpy(host).cuda(), torch.zeros(64, dtype=torch.uint8, device="cuda")])
-rng = np.random.default_rng(5)
-tabs, wants, outs, graphs = [], [], [], []
-for k in range(2):
-    offs = np.zeros(3001, dtype=np.uint64)
-    offs[1:] = np.cumsum(rng.integers(0, 2600, 3000))
-    tabs.append(torch.from_numpy(offs.astype(np.int64)).cuda())
-    wants.append(O.batch_offsets("crc32c", host, offs, nthreads=8))
-    outs.append(torch.zeros(3000, dtype=torch.int32, device="cuda"))
-G.prepare("crc32c")
-torch.cuda.synchronize()
-streams = [torch.cuda.Stream(), torch.cuda.Stream()]
-for k in range(2):
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.stream(streams[k]), torch.cuda.graph(g, stream=streams[k]):
-        G.checksum_offsets("crc32c", dev, tabs[k], out=outs[k])
-    graphs.append(g)
-torch.cuda.synchronize()
-bad = 0
-for rep in range(200):
+def test_captured_launches_replayed_concurrently_stay_correct(gpu, oracle_mod, monkeypatch):
+    """Graph-captured launches get no work-queue slot and take the static split
+    (crc_gpu_device.h, "Exclusivity"): two offsets graphs, a split CRC-64 graph
+    (pieces XORed into a zeroed output, MCHECKSUM_GPU_SPLIT=1) and a
+    scatter-gather graph (chunks XORed into out[]) replayed at the same time on
+    four streams, next to eager queue launches on a fifth, keep returning the
+    oracle's values.  (Round 2's shared-slot ownership failed this: a replay
+    whose early workgroups found the slot busy and later ones found it free
+    never released it, and its next replay skipped units -- 1 bad batch in 400.)"""
+    import torch
+    G, O = gpu, oracle_mod
+    monkeypatch.setenv("MCHECKSUM_GPU_LIGHT", "0")
+    host = O.splitmix_bytes(8 << 20, 31337)
+    dev = torch.cat([torch.from_numpy(host).cuda(), torch.zeros(64, dtype=torch.uint8, device="cuda")])
+    rng = np.random.default_rng(5)
+    tabs, wants, outs = [], [], []
     for k in range(2):
-        outs[k].zero_()
+        offs = np.zeros(3001, dtype=np.uint64)
+        offs[1:] = np.cumsum(rng.integers(0, 2600, 3000))
+        tabs.append(torch.from_numpy(offs.astype(np.int64)).cuda())
+        wants.append(O.batch_offsets("crc32c", host, offs, nthreads=8))
+        outs.append(torch.zeros(3000, dtype=torch.int32, device="cuda"))
+    # split CRC-64: 16 payloads of 512 KiB (2 pieces each)
+    want_sp = O.batch_fixed("crc64", host, 512 << 10, 512 << 10, 16, nthreads=8)
+    out_sp = torch.zeros(16, dtype=torch.int64, device="cuda")
+    # scatter-gather: 24 objects of 3 segments (256 KiB + 40 KiB + 4 KiB) from anywhere
+    seg_lens = [256 << 10, 40 << 10, 4 << 10]
+    starts = rng.integers(0, (8 << 20) - (256 << 10), 72) // 16 * 16
+    segs = [dev[int(a):int(a) + seg_lens[q % 3]] for q, a in enumerate(starts)]
+    batch = G.SegmentBatch(segs, np.arange(0, 73, 3))
+    want_sg = [O.crc("crc64", np.concatenate([host[int(starts[3 * j + q]):int(starts[3 * j + q]) + seg_lens[q]]
+                                               for q in range(3)])) for j in range(24)]
+    out_sg = torch.zeros(24, dtype=torch.int64, device="cuda")
+    G.prepare("crc32c")
+    G.prepare("crc64")
     torch.cuda.synchronize()
-    for k in range(2):
-        with torch.cuda.stream(streams[k]):
-            graphs[k].replay()
+    streams = [torch.cuda.Stream() for _ in range(5)]
+    calls = [lambda: G.checksum_offsets("crc32c", dev, tabs[0], out=outs[0]),
+             lambda: G.checksum_offsets("crc32c", dev, tabs[1], out=outs[1]),
+             lambda: G.checksum_fixed("crc64", dev, 512 << 10, count=16, out=out_sp),
+             lambda: batch.checksum("crc64", out=out_sg)]
+    graphs = []
+    monkeypatch.setenv("MCHECKSUM_GPU_SPLIT", "1")
+    for k, f in enumerate(calls):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(streams[k]), torch.cuda.graph(g, stream=streams[k]):
+            f()
+        graphs.append(g)
     torch.cuda.synchronize()
-    for k in range(2):
-        bad += int(not np.array_equal(G.as_unsigned(outs[k]).astype(np.uint64), wants[k]))
-print("bad", bad, "faults", G.queue_faults(), flush=True)
-sys.exit(0 if bad == 0 and G.queue_faults() == 0 else 1)
-"""
-    env = dict(os.environ, MCHECKSUM_GPU_CAPTURED_SLOTS="1", MCHECKSUM_GPU_LIGHT="0",
-               ROOT=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110)
-    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    eager_out = torch.zeros(3000, dtype=torch.int32, device="cuda")
+    bad = {"offsets0": 0, "offsets1": 0, "split64": 0, "segments": 0, "eager": 0}
+    for rep in range(150):
+        for o in outs + [out_sp, out_sg, eager_out]:
+            o.zero_()
+        torch.cuda.synchronize()
+        for k, g in enumerate(graphs):
+            with torch.cuda.stream(streams[k]):
+                g.replay()
+        with torch.cuda.stream(streams[4]):
+            G.checksum_offsets("crc32c", dev, tabs[rep % 2], out=eager_out, stream=streams[4])
+        _wait(torch, ("captured", rep), streams)
+        for k in range(2):
+            bad[f"offsets{k}"] += int(not np.array_equal(G.as_unsigned(outs[k]).astype(np.uint64), wants[k]))
+        bad["split64"] += int(not np.array_equal(G.as_unsigned(out_sp), want_sp))
+        bad["segments"] += int(not np.array_equal(G.as_unsigned(out_sg), np.asarray(want_sg, dtype=np.uint64)))
+        bad["eager"] += int(not np.array_equal(G.as_unsigned(eager_out).astype(np.uint64), wants[rep % 2]))
+    assert sum(bad.values()) == 0 and G.queue_faults() == 0, bad

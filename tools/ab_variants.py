@@ -26,6 +26,7 @@ SHAPES = {
     "c4": ("crc32c", 262144, None, 0x4D43310000000004),   # offsets table, U[64 B, 64 KiB]
     "c4_64": ("crc64", 262144, None, 0x4D43310000000004),
     "seg": ("crc64", 8192, "seg", 0x4D43310000000003),      # bench.py's segments layout
+    "seg32": ("crc32c", 8192, "seg", 0x4D43310000000003),   # the same layout, CRC-32C
 }
 
 
