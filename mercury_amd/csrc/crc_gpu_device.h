@@ -848,10 +848,11 @@ __device__ __forceinline__ uint32_t payload32_generic(TAB lds, const crc32_gpu_p
     const int64_t kmax = LOG2G == 6 ? K : wave_max(K);
     const int64_t lane_off = 16 * (int64_t)gl;
 
+    const gbyte_t g0 = global_ptr(reinterpret_cast<const uint8_t *>(a0), false);
     auto fetch = [&](int64_t k) -> uint4 {
         const int64_t pc = r0 + k * step + lane_off;
         uint4 v = make_uint4(0, 0, 0, 0);
-        if (k < K && pc >= 0) v = ld16<NT>(reinterpret_cast<const uint4 *>(a0 + (uint64_t)pc));
+        if (k < K && pc >= 0) v = ldg16<NT>(g0 + (uint64_t)pc);
         return v;
     };
     // edge handling (crc_gpu_mask.h) for the piece of step k < K
@@ -907,7 +908,7 @@ __device__ __forceinline__ uint32_t payload32_g64(TAB lds, const crc32_gpu_pack_
     const uint32_t W = (uint32_t)(a1 - a0);
     const uint32_t K = (W + 1023u) >> 10;
     const uint32_t lead = K * 1024u - W;                 // window starts `lead` bytes into step 0
-    const uint8_t *wb = reinterpret_cast<const uint8_t *>(a0 - lead);  // step grid origin (uniform)
+    const gbyte_t wb = global_ptr(reinterpret_cast<const uint8_t *>(a0 - lead), true);  // step grid origin
     const uint32_t qs = lead + (uint32_t)(sa - a0);      // payload [qs, qe) relative to wb
     const uint32_t qe = lead + (uint32_t)(ea - a0);
     const int32_t ilen = (int32_t)len;
@@ -915,37 +916,45 @@ __device__ __forceinline__ uint32_t payload32_g64(TAB lds, const crc32_gpu_pack_
     // steps [kc0, kc1) are clean for every lane
     const uint32_t kc0 = (qs + 4u + 1023u) >> 10;
     const uint32_t kc1 = qe >= 1024u ? (qe - 1024u) / 1024u + 1u : 0u;
-
-    auto fetch = [&](uint32_t k) -> uint4 {
-        const uint32_t q = k * 1024u + lo_lane;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (k < K && q >= lead) v = ld16<NT>(reinterpret_cast<const uint4 *>(wb + q));
-        return v;
-    };
+    constexpr uint32_t R = kRingOff;
 
     uint32_t x0 = 0, x1 = 0, x2 = 0, x3 = 0;
-    uint4 ring[kRingOff];
+    auto fold = [&](uint32_t kk, uint4 v) {
+        if (kk < kc0 || kk >= kc1) {  // wave-uniform: an edge step
+            const int32_t lo = (int32_t)(kk * 1024u + lo_lane) - (int32_t)qs;
+            v.x = mck_mask32(v.x, lo, ilen, init);
+            v.y = mck_mask32(v.y, lo + 4, ilen, init);
+            v.z = mck_mask32(v.z, lo + 8, ilen, init);
+            v.w = mck_mask32(v.w, lo + 12, ilen, init);
+        }
+        x0 = f32s(lds, x0 ^ v.x, lc0, lc1);
+        x1 = f32s(lds, x1 ^ v.y, lc0, lc1);
+        x2 = f32s(lds, x2 ^ v.z, lc0, lc1);
+        x3 = f32s(lds, x3 ^ v.w, lc0, lc1);
+    };
+    // Loads go through global (address-space 1) pointers -- flat loads would
+    // also count against lgkmcnt, so every LDS wait of the fold would wait for
+    // the ring's HBM loads too -- and only step 0 tests lanes (the ones before
+    // the window start read nothing); the steady loop loads unconditionally.
+    uint4 ring[R];
+    ring[0] = K > 0 && lo_lane >= lead ? ldg16<NT>(wb + lo_lane) : make_uint4(0, 0, 0, 0);
 #pragma unroll
-    for (int u = 0; u < kRingOff; u++) ring[u] = fetch(u);
-    for (uint32_t k = 0; k < K; k += kRingOff) {
+    for (uint32_t u = 1; u < R; u++) ring[u] = u < K ? ldg16<NT>(wb + (u * 1024u + lo_lane)) : make_uint4(0, 0, 0, 0);
+    uint32_t k = 0;
+    for (; k + 2 * R <= K; k += R) {
 #pragma unroll
-        for (int u = 0; u < kRingOff; u++) {
-            uint4 v = ring[u];
-            const uint32_t kk = k + u;
-            ring[u] = fetch(kk + kRingOff);
-            if (kk < K) {
-                if (kk < kc0 || kk >= kc1) {  // wave-uniform: an edge step
-                    const int32_t lo = (int32_t)(kk * 1024u + lo_lane) - (int32_t)qs;
-                    v.x = mck_mask32(v.x, lo, ilen, init);
-                    v.y = mck_mask32(v.y, lo + 4, ilen, init);
-                    v.z = mck_mask32(v.z, lo + 8, ilen, init);
-                    v.w = mck_mask32(v.w, lo + 12, ilen, init);
-                }
-                x0 = f32s(lds, x0 ^ v.x, lc0, lc1);
-                x1 = f32s(lds, x1 ^ v.y, lc0, lc1);
-                x2 = f32s(lds, x2 ^ v.z, lc0, lc1);
-                x3 = f32s(lds, x3 ^ v.w, lc0, lc1);
-            }
+        for (uint32_t u = 0; u < R; u++) {
+            const uint4 v = ring[u];
+            ring[u] = ldg16<NT>(wb + ((k + u + R) * 1024u + lo_lane));
+            fold(k + u, v);
+        }
+    }
+    for (; k < K; k += R) {
+#pragma unroll
+        for (uint32_t u = 0; u < R; u++) {
+            const uint4 v = ring[u];
+            if (k + u + R < K) ring[u] = ldg16<NT>(wb + ((k + u + R) * 1024u + lo_lane));
+            if (k + u < K) fold(k + u, v);
         }
     }
     uint32_t x = combine32<6>(lds, x0, x1, x2, x3, gl);
@@ -1352,10 +1361,12 @@ __device__ __forceinline__ uint64_t payload64_aligned(const uint8_t *lds, const 
     constexpr int G = 1 << LOG2G;
     constexpr int R = kRing;
     Lane64 ln = lane64(lc);
-    const uint4 *src = reinterpret_cast<const uint4 *>(p) + gl;
+    // global (address-space 1) loads: a flat load would also hold up every LDS wait
+    const gbyte_t src = global_ptr(p, LOG2G == 6) + 16u * gl;
+    auto ldk = [&](uint32_t k) { return ldg16<NT>(src + (uint64_t)k * (16u * G)); };
     uint4 ring[R];
 #pragma unroll
-    for (int u = 0; u < R; u++) ring[u] = (uint32_t)u < K ? ld16<NT>(src + (uint64_t)u * G) : make_uint4(0, 0, 0, 0);
+    for (int u = 0; u < R; u++) ring[u] = (uint32_t)u < K ? ldk(u) : make_uint4(0, 0, 0, 0);
 #if MCK_LA64
     // x holds state ^ (the data word of the step about to run)
     uint64_t x0 = (gl == 0 ? init : 0ull) ^ lo64(ring[0]), x1 = hi64(ring[0]);
@@ -1363,7 +1374,7 @@ __device__ __forceinline__ uint64_t payload64_aligned(const uint8_t *lds, const 
     for (; k + 2 * R <= K; k += R) {  // every load and look-ahead in range
 #pragma unroll
         for (int u = 0; u < R; u++) {
-            ring[u] = ld16<NT>(src + (uint64_t)(k + u + R) * G);
+            ring[u] = ldk(k + u + R);
             const uint4 nx = ring[(u + 1) % R];
             x0 = f64x(lds, x0, lo64(nx), ln);
             x1 = f64x(lds, x1, hi64(nx), ln);
@@ -1372,7 +1383,7 @@ __device__ __forceinline__ uint64_t payload64_aligned(const uint8_t *lds, const 
     for (; k < K; k += R) {
 #pragma unroll
         for (int u = 0; u < R; u++) {
-            if (k + u + R < K) ring[u] = ld16<NT>(src + (uint64_t)(k + u + R) * G);
+            if (k + u + R < K) ring[u] = ldk(k + u + R);
             if (k + u < K) {
                 const uint4 nx = k + u + 1 < K ? ring[(u + 1) % R] : make_uint4(0, 0, 0, 0);
                 x0 = f64x(lds, x0, lo64(nx), ln);
@@ -1387,7 +1398,7 @@ __device__ __forceinline__ uint64_t payload64_aligned(const uint8_t *lds, const 
         for (int u = 0; u < R; u++) {
             const uint4 v = ring[u];
             const uint32_t kn = k + u + R;
-            if (kn < K) ring[u] = ld16<NT>(src + (uint64_t)kn * G);
+            if (kn < K) ring[u] = ldk(kn);
             if (k + u < K) {
                 x0 = f64x(lds, x0 ^ lo64(v), 0, ln);
                 x1 = f64x(lds, x1 ^ hi64(v), 0, ln);
@@ -1414,10 +1425,11 @@ __device__ __forceinline__ uint64_t payload64_generic(const uint8_t *lds, const 
     const int64_t kmax = LOG2G == 6 ? K : wave_max(K);
     const int64_t lane_off = 16 * (int64_t)gl;
 
+    const gbyte_t g0 = global_ptr(reinterpret_cast<const uint8_t *>(a0), false);
     auto fetch = [&](int64_t k) -> uint4 {
         const int64_t pc = r0 + k * step + lane_off;
         uint4 v = make_uint4(0, 0, 0, 0);
-        if (k < K && pc >= 0) v = ld16<NT>(reinterpret_cast<const uint4 *>(a0 + (uint64_t)pc));
+        if (k < K && pc >= 0) v = ldg16<NT>(g0 + (uint64_t)pc);
         return v;
     };
     // edge handling (crc_gpu_mask.h) for the piece of step k < K
@@ -1467,42 +1479,46 @@ __device__ __forceinline__ uint64_t payload64_g64(const uint8_t *lds, const crc6
     const uint32_t W = (uint32_t)(a1 - a0);
     const uint32_t K = (W + 1023u) >> 10;
     const uint32_t lead = K * 1024u - W;
-    const uint8_t *wb = reinterpret_cast<const uint8_t *>(a0 - lead);
+    const gbyte_t wb = global_ptr(reinterpret_cast<const uint8_t *>(a0 - lead), true);
     const uint32_t qs = lead + (uint32_t)(sa - a0);
     const uint32_t qe = lead + (uint32_t)(ea - a0);
     const int32_t ilen = (int32_t)len;
     const uint32_t lo_lane = 16u * gl;
     const uint32_t kc0 = (qs + 8u + 1023u) >> 10;
     const uint32_t kc1 = qe >= 1024u ? (qe - 1024u) / 1024u + 1u : 0u;
-
-    auto fetch = [&](uint32_t k) -> uint4 {
-        const uint32_t q = k * 1024u + lo_lane;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (k < K && q >= lead) v = ld16<NT>(reinterpret_cast<const uint4 *>(wb + q));
-        return v;
-    };
+    constexpr uint32_t R = kRingOff64;
 
     uint64_t x0 = 0, x1 = 0;
     Lane64 ln = lane64(lc);
-    uint4 ring[kRingOff64];
+    auto fold = [&](uint32_t kk, uint4 v) {
+        uint64_t w0 = lo64(v), w1 = hi64(v);
+        if (kk < kc0 || kk >= kc1) {  // wave-uniform: an edge step
+            const int32_t lo = (int32_t)(kk * 1024u + lo_lane) - (int32_t)qs;
+            w0 = mck_mask64(w0, lo, ilen, init);
+            w1 = mck_mask64(w1, lo + 8, ilen, init);
+        }
+        x0 = f64x(lds, x0 ^ w0, 0, ln);
+        x1 = f64x(lds, x1 ^ w1, 0, ln);
+    };
+    uint4 ring[R];
+    ring[0] = K > 0 && lo_lane >= lead ? ldg16<NT>(wb + lo_lane) : make_uint4(0, 0, 0, 0);
 #pragma unroll
-    for (int u = 0; u < kRingOff64; u++) ring[u] = fetch(u);
-    for (uint32_t k = 0; k < K; k += kRingOff64) {
+    for (uint32_t u = 1; u < R; u++) ring[u] = u < K ? ldg16<NT>(wb + (u * 1024u + lo_lane)) : make_uint4(0, 0, 0, 0);
+    uint32_t k = 0;
+    for (; k + 2 * R <= K; k += R) {
 #pragma unroll
-        for (int u = 0; u < kRingOff64; u++) {
+        for (uint32_t u = 0; u < R; u++) {
             const uint4 v = ring[u];
-            const uint32_t kk = k + u;
-            ring[u] = fetch(kk + kRingOff64);
-            if (kk < K) {
-                uint64_t w0 = lo64(v), w1 = hi64(v);
-                if (kk < kc0 || kk >= kc1) {
-                    const int32_t lo = (int32_t)(kk * 1024u + lo_lane) - (int32_t)qs;
-                    w0 = mck_mask64(w0, lo, ilen, init);
-                    w1 = mck_mask64(w1, lo + 8, ilen, init);
-                }
-                x0 = f64x(lds, x0 ^ w0, 0, ln);
-                x1 = f64x(lds, x1 ^ w1, 0, ln);
-            }
+            ring[u] = ldg16<NT>(wb + ((k + u + R) * 1024u + lo_lane));
+            fold(k + u, v);
+        }
+    }
+    for (; k < K; k += R) {
+#pragma unroll
+        for (uint32_t u = 0; u < R; u++) {
+            const uint4 v = ring[u];
+            if (k + u + R < K) ring[u] = ldg16<NT>(wb + ((k + u + R) * 1024u + lo_lane));
+            if (k + u < K) fold(k + u, v);
         }
     }
     uint64_t x = combine64<6, OM>(lds, pk, x0, x1, gl);
