@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
 #include "crc_gpu_layout.h"
 #include "crc_gpu_mask.h"
@@ -35,9 +36,11 @@ constexpr int kRing = MCK_RING;  // dwordx4 pieces in flight per lane
 #endif
 constexpr int kRingOff = MCK_RING_OFFSETS;
 
-// CRC-32C LDS map: [0,128K) main byte tables x32 copies; then op nibble tables.
+// CRC-32C LDS map: [0,128K) main byte tables x32 copies; then op nibble
+// tables; then the two-level combine operators (crc_gpu_layout.h lv, 8 KiB).
 constexpr uint32_t kL32Main = 131072;
-constexpr uint32_t kL32Bytes = kL32Main + CRC32_NOPS_MAX * 512;
+constexpr uint32_t kL32Lv = kL32Main + CRC32_NOPS_MAX * 512;
+constexpr uint32_t kL32Bytes = kL32Lv + 2 * 8 * 16 * 8 * 4;
 // Light layout for small batches: the 4 byte tables unreplicated (4 KiB, so
 // the per-workgroup LDS fill is 16 KiB instead of 140 KiB) and 256-thread
 // workgroups spread over every CU; lookups may bank-conflict, which a small
@@ -650,12 +653,41 @@ __device__ __forceinline__ uint32_t op32(Tab32<LIGHT> tab, uint32_t o, uint32_t 
     return xor3(xor3(t[0], t[1], t[2]), xor3(t[3], t[4], t[5]), t[6] ^ t[7]);
 }
 
+// Lane-dependent operator i of level l of the two-level combine (LDS map
+// above; interleaved so that lanes with different i hit different banks).
+__device__ __forceinline__ uint32_t oplv32(Tab32<false> tab, uint32_t l, uint32_t i, uint32_t x) {
+    const uint32_t base = kL32Lv + l * 4096 + i * 4;
+    uint32_t t[8];
+#pragma unroll
+    for (int h = 0; h < 8; h++) t[h] = lds32(tab.lds, base + h * 512 + (((x >> (4 * h)) & 15u) << 5));
+    return xor3(xor3(t[0], t[1], t[2]), xor3(t[3], t[4], t[5]), t[6] ^ t[7]);
+}
+
+// XOR_q Z^(-4q)(S_q) in the lane, then over the G lanes of the group.  For
+// G = 64 on the throughput layout (MCK_LV32): lane l = 8a + b applies
+// Z^(-16b), the 8 lanes of each a XOR-reduce (shuffles only), the groups
+// apply Z^(-128a) and XOR-reduce -- two table operators on the lane's path
+// instead of six butterfly levels of one each.
+#ifndef MCK_LV32
+#define MCK_LV32 1
+#endif
 template <int LOG2G, class TAB>
 __device__ __forceinline__ uint32_t combine32(TAB lds, uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3,
                                               uint32_t gl) {
     uint32_t x = s0 ^ op32(lds, 0, s1);
     const uint32_t y = s2 ^ op32(lds, 0, s3);
     x ^= op32(lds, 1, y);
+    if constexpr (MCK_LV32 && LOG2G == 6 && std::is_same<TAB, Tab32<false>>::value) {
+        x = oplv32(lds, 0, gl & 7u, x);
+        x ^= __shfl_xor(x, 1, 64);
+        x ^= __shfl_xor(x, 2, 64);
+        x ^= __shfl_xor(x, 4, 64);
+        x = oplv32(lds, 1, gl >> 3, x);
+        x ^= __shfl_xor(x, 8, 64);
+        x ^= __shfl_xor(x, 16, 64);
+        x ^= __shfl_xor(x, 32, 64);
+        return x;
+    }
 #pragma unroll
     for (int k = 0; k < LOG2G; k++) {
         const uint32_t other = __shfl_xor(x, 1 << k, 64);
@@ -687,6 +719,10 @@ __device__ void fill_lds32(uint8_t *lds, const crc32_gpu_pack_t *pk) {
     const uint32_t nops = pk->nops * 32u;
     const uint32_t base = (LIGHT ? kL32LightMain : kL32Main) / 16;
     for (uint32_t q = threadIdx.x; q < nops; q += BLOCK) l4[base + q] = ops[q];
+    if constexpr (!LIGHT) {  // two-level combine operators (used at G = 64)
+        const uint4 *lv = reinterpret_cast<const uint4 *>(&pk->lv[0][0][0][0]);
+        for (uint32_t q = threadIdx.x; q < 512u; q += BLOCK) l4[kL32Lv / 16 + q] = lv[q];
+    }
 }
 
 // Ring slot j % kRing holds the piece of step j, loaded kRing steps ahead.

@@ -33,6 +33,13 @@ typedef struct {
     uint32_t init;
     uint32_t log2g;
     uint32_t nops;
+    /* Two-level lane combine (log2g == 6 only): XOR_l Z^(-16 l)(v_l) over the
+     * 64 lanes as Z^(-128 a) o Z^(-16 b), l = 8a + b -- one lane-dependent
+     * operator per level instead of six butterfly levels.  Interleaved
+     * [level][h][v][i] = M_{level,i}(v << 4h), M_{0,i} = Z^(-16 i),
+     * M_{1,i} = Z^(-128 i), so lanes with different operators i read
+     * different LDS banks.                                                   */
+    uint32_t lv[2][8][16][8];
 } crc32_gpu_pack_t;
 
 /* ---- CRC-64 (W = 64): nibble tables, 16 per step, 32-bank replicated ---- */

@@ -209,6 +209,17 @@ crc32_gpu_pack_build(const crc_rmodel_t *m, int log2g, crc32_gpu_pack_t *out)
             return -1;
         out->zinit[k] = (uint32_t) crc_op_apply(32, op, m->rinit);
     }
+    if (log2g == 6) {
+        int lvl, i, h, v;
+        for (lvl = 0; lvl < 2; lvl++)
+            for (i = 0; i < 8; i++) {
+                if (crc_op_zpow(m, -(int64_t) i * (lvl ? 128 : 16), op) != 0)
+                    return -1;
+                for (h = 0; h < 8; h++)
+                    for (v = 0; v < 16; v++)
+                        out->lv[lvl][h][v][i] = (uint32_t) crc_op_apply(32, op, (uint64_t) v << (4 * h));
+            }
+    }
     out->xorout = (uint32_t) m->xorout;
     out->init = (uint32_t) m->rinit;
     out->log2g = (uint32_t) log2g;

@@ -64,15 +64,31 @@ extern "C" uint32_t emu_crc32(const crc32_gpu_pack_t *pk, const uint8_t *buf, in
         uint32_t b = S[4 * l + 2] ^ op32(*pk, 0, S[4 * l + 3]);
         X[l] = a ^ op32(*pk, 1, b);
     }
-    for (int k = 0; k < log2g; k++) {  // butterfly, as the shuffles do it
-        std::vector<uint32_t> Y(G);
-        for (int l = 0; l < G; l++) {
-            uint32_t other = X[l ^ (1 << k)];
-            bool bit = (l >> k) & 1;
-            uint32_t lo = bit ? other : X[l], hi = bit ? X[l] : other;
-            Y[l] = lo ^ op32(*pk, 2 + k, hi);
+    if (log2g == 6 && !getenv("EMU_BUTTERFLY")) {  // two-level combine (throughput layout, G = 64)
+        uint32_t acc = 0;
+        for (int a = 0; a < 8; a++) {
+            uint32_t grp = 0;
+            for (int b = 0; b < 8; b++) {
+                uint32_t r = 0;
+                for (int h = 0; h < 8; h++) r ^= pk->lv[0][h][(X[8 * a + b] >> (4 * h)) & 15][b];
+                grp ^= r;
+            }
+            uint32_t r = 0;
+            for (int h = 0; h < 8; h++) r ^= pk->lv[1][h][(grp >> (4 * h)) & 15][a];
+            acc ^= r;
         }
-        X = Y;
+        X[0] = acc;
+    } else {
+        for (int k = 0; k < log2g; k++) {  // butterfly, as the shuffles do it
+            std::vector<uint32_t> Y(G);
+            for (int l = 0; l < G; l++) {
+                uint32_t other = X[l ^ (1 << k)];
+                bool bit = (l >> k) & 1;
+                uint32_t lo = bit ? other : X[l], hi = bit ? X[l] : other;
+                Y[l] = lo ^ op32(*pk, 2 + k, hi);
+            }
+            X = Y;
+        }
     }
     uint32_t r = op32(*pk, 2 + log2g + (int)t, X[0]);
     if (len < 4) r ^= pk->zinit[len];
