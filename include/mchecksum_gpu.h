@@ -31,7 +31,9 @@
  * overlap).  Calls captured into a hipGraph, calls on hipStreamPerThread and
  * streams past the 2048th take a static split of the batch instead: a graph
  * replays its captured arguments, possibly on two execs at once, so no slot
- * could be exclusive to it.
+ * could be exclusive to it.  The slot is keyed by the stream handle: a stream
+ * destroyed with calls still in flight must be synchronized first if a new
+ * stream may receive the same handle (its launches would share the slot).
  *
  * Fail closed: every wait in the work queue is bounded.  A launch in which a
  * wait gives up (a protocol fault; 0 in every test run) adds 1 to the error
