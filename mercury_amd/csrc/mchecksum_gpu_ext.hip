@@ -58,6 +58,11 @@ struct SegArgs {
     uint64_t nobj;
     const uint64_t *P, *C;  // workspace: byte / chunk exclusive prefix sums, nseg + 1 each
     const unsigned long long *ragged;  // workspace: non-zero if any chunk needs the ragged loop
+    // workspace: object of each segment (kNoObj outside [first[0], first[nobj]))
+    // and the segment of each chunk while the chunks fit map_cap
+    const uint64_t *obj;
+    const uint32_t *map;
+    uint64_t map_cap;
     void *out;
     const void *pack, *shift;
     // work-queue slot of the chunk passes (crc_gpu_device.h, WgQueue; nullptr:
@@ -176,8 +181,12 @@ __global__ __launch_bounds__(kScanThreads) void seg_scan_top(uint64_t *tot, uint
     }
 }
 
+constexpr uint64_t kNoObj = ~0ull;
+
 __global__ __launch_bounds__(kScanThreads) void seg_scan_down(const uint64_t *len, uint64_t nseg, const uint64_t *tot,
-                                                              uint64_t *P, uint64_t *C) {
+                                                              uint64_t *P, uint64_t *C, const uint64_t *first,
+                                                              uint64_t nobj, uint64_t *obj, uint32_t *map,
+                                                              uint64_t map_cap) {
     uint64_t l[kScanPer], p = 0, c = 0;
 #pragma unroll
     for (uint32_t e = 0; e < kScanPer; e++) {
@@ -190,12 +199,22 @@ __global__ __launch_bounds__(kScanThreads) void seg_scan_down(const uint64_t *le
     uint64_t tp, tc;
     block_scan2(p, c, &tp, &tc);
     uint64_t ep = tot[3 * blockIdx.x] + p - p0, ec = tot[3 * blockIdx.x + 1] + c - c0;
+    const uint64_t f0 = first[0], f1 = first[nobj];
 #pragma unroll
     for (uint32_t e = 0; e < kScanPer; e++) {
         const uint64_t i = (uint64_t)blockIdx.x * kScanBlk + threadIdx.x * kScanPer + e;
         if (i < nseg) {
             P[i] = ep;
             C[i] = ec;
+            // the object holding segment i: the last j with first[j] <= i
+            // (empty objects before it share its first index); only the
+            // queue pass reads it (nullptr otherwise)
+            if (obj) obj[i] = i >= f0 && i < f1 ? lower_bound_u64(first, nobj + 1, i + 1) - 1 : kNoObj;
+            // chunk -> segment map, while it fits (the chunk passes check the
+            // total against map_cap and search C otherwise)
+            const uint64_t ce = ec + seg_chunks(l[e]);
+            if (ce <= map_cap)
+                for (uint64_t k = ec; k < ce; k++) map[k] = (uint32_t)i;
         }
         ep += l[e];
         ec += seg_chunks(l[e]);
@@ -244,63 +263,33 @@ struct ChunkWalk {
     }
 };
 
-// Work-queue chunk passes (MCK_SEG_QUEUE=1, an A/B build): chunks are the
-// queue's units, so a wave holds chunks from anywhere in the list and finds
-// each one's segment and object by search.  The guess (chunk index scaled by
-// segments per chunk, segment index by objects per segment) is exact for
-// uniform segment and object sizes -- two scalar loads -- and a gallop +
-// binary search bounds the rest.  Measured against the static contiguous
-// ranges: `seg` (CRC-64) 1.515 vs 1.439 ms, CRC-32C 1.301 vs 1.295 ms
-// (profiles/r02/ab_seg_queue.log) -- so the default stays static.
+// Work-queue chunk passes.  Chunks are the queue's units, so a wave holds
+// chunks from anywhere in the list and needs each one's segment and object
+// without walking: the scan writes both maps (SegArgs::obj, ::map), so a
+// chunk costs three dependent scalar loads.  A list with more chunks than the
+// map holds (segments far above 1 MiB on average) searches C instead.
+// The first build searched C and first[] for every chunk (a guess plus a
+// gallop): its search loops pushed the 64-VGPR CRC-64 pass into 54 SGPR / 10
+// VGPR spills and it measured 5% slower than the static ranges
+// (profiles/r02/ab_seg_queue.log).  MCK_SEG_QUEUE=0 builds the static
+// contiguous ranges (ChunkWalk) for the A/B.
 #ifndef MCK_SEG_QUEUE
-#define MCK_SEG_QUEUE 0
+#define MCK_SEG_QUEUE 1
 #endif
 
-// The last i in [0, n) with A[i] <= key, for non-decreasing A with
-// A[0] <= key < A[n] (n >= 1), searched from the guess g.
-__device__ uint64_t seg_find(const uint64_t *A, uint64_t n, uint64_t key, uint64_t g) {
-    uint64_t lo, hi;  // A[lo] <= key < A[hi]
-    g = g < n ? g : n - 1;
-    if (A[g] <= key) {
-        lo = g;
-        hi = g + 1;
-        for (uint64_t step = 1; hi < n && A[hi] <= key; step <<= 1) {
-            lo = hi;
-            hi = n - lo > 2 * step ? lo + 2 * step : n;
-        }
-    } else {
-        hi = g;
-        lo = g - 1;  // g >= 1 here: A[0] <= key
-        for (uint64_t step = 1; lo > 0 && A[lo] > key; step <<= 1) {
-            hi = lo;
-            lo = lo > 2 * step ? lo - 2 * step : 0;
-        }
-    }
-    while (hi - lo > 1) {
-        const uint64_t mid = lo + (hi - lo) / 2;
-        if (A[mid] <= key) lo = mid;
-        else hi = mid;
-    }
-    return lo;
-}
-
-__device__ __forceinline__ uint64_t seg_guess(uint64_t i, uint64_t n, uint64_t total) {
-    return total ? (uint64_t)((double)i * (double)n / (double)total) : 0;
-}
-
-// Chunk c (< C[nseg]): its bytes [addr, addr + n) and, when its segment
+// Chunk c (< nchunks): its bytes [addr, addr + n) and, when its segment
 // belongs to an object (*in), the object and the object bytes after it.
 // c is wave-uniform, so every load is scalar.
-__device__ __forceinline__ __attribute__((unused)) void seg_locate(const SegArgs &a, uint64_t c, uint64_t nchunks, uint64_t *addr, uint64_t *n,
-                                           bool *in, uint64_t *obj, uint64_t *after) {
-    const uint64_t s = seg_find(a.C, a.nseg, c, seg_guess(c, a.nseg, nchunks));
+__device__ __forceinline__ __attribute__((unused)) void seg_locate(const SegArgs &a, uint64_t c, uint64_t nchunks,
+                                                                   uint64_t *addr, uint64_t *n, bool *in,
+                                                                   uint64_t *obj, uint64_t *after) {
+    const uint64_t s = nchunks <= a.map_cap ? (uint64_t)a.map[c] : lower_bound_u64(a.C, a.nseg + 1, c + 1) - 1;
     const uint64_t off = (c - a.C[s]) * kChunk, L = a.len[s];
     *addr = a.addr[s] + off;
     *n = L - off < kChunk ? L - off : kChunk;
-    const uint64_t f0 = a.first[0], f1 = a.first[a.nobj];
-    *in = s >= f0 && s < f1;
+    const uint64_t j = a.obj[s];
+    *in = j != kNoObj;
     if (*in) {
-        const uint64_t j = seg_find(a.first, a.nobj, s, seg_guess(s - f0, a.nobj, f1 - f0));
         *obj = j;
         *after = a.P[a.first[j + 1]] - (a.P[s] + off + *n);
     }
@@ -349,8 +338,9 @@ __global__ __launch_bounds__(1024, kSegWavesPerEU<W * 4 + PART>) void seg_kernel
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWPB + (threadIdx.x >> 6));
     const uint32_t nw = gridDim.x * kWPB;
     const uint64_t nchunks = uniform(a.C[a.nseg]);
-    // chunk passes with the work queue: PART 0 and PART 1 (the host passes a slot)
-    constexpr bool kQueue = MCK_SEG_QUEUE && PART != 2;
+    // the CRC-64 aligned chunk pass takes chunks from the work queue (the host
+    // passes a slot; without one, for_each_unit strides statically)
+    constexpr bool kQueue = MCK_SEG_QUEUE && PART == 1;
     __shared__ WgQueue wgq;
     if (kQueue && threadIdx.x == 0) wg_queue_init(&wgq, a.queue, nchunks);
     // Calls body(addr, n, j, after) for every chunk of this wave that belongs
@@ -675,13 +665,18 @@ using namespace mck;
 
 extern "C" {
 
-// P, C (nseg + 1 each), the ragged flag (+ pad), 3 words per scan block.
-// More than 2^40 segments (far beyond device memory) is rejected, so the size
-// cannot wrap: SIZE_MAX then makes any allocation of it fail.
+// P, C (nseg + 1 each), the ragged flag (+ pad), 3 words per scan block, the
+// object of each segment (nseg), then the chunk -> segment map (u32 entries:
+// 4 per segment + 64 Ki, i.e. lists averaging up to ~1 MiB per segment, or
+// one huge segment up to 16 GiB; none past 2^32 segments).  More than 2^40
+// segments (far beyond device memory) is rejected, so the size cannot wrap:
+// SIZE_MAX then makes any allocation of it fail.
 constexpr uint64_t kMaxSegs = 1ull << 40;
+uint64_t seg_map_cap(uint64_t nseg) { return nseg < (1ull << 32) ? 4 * nseg + 65536 : 0; }
+uint64_t seg_words(uint64_t nseg) { return 2 * (nseg + 1) + 2 + 3 * ((nseg + kScanBlk - 1) / kScanBlk) + nseg; }
 size_t mchecksum_gpu_segments_work_size(size_t nseg) {
     if ((uint64_t)nseg > kMaxSegs) return SIZE_MAX;
-    return sizeof(uint64_t) * (2 * (nseg + 1) + 2 + 3 * ((nseg + kScanBlk - 1) / kScanBlk));
+    return sizeof(uint64_t) * seg_words(nseg) + sizeof(uint32_t) * seg_map_cap(nseg);
 }
 
 int mchecksum_gpu_checksum_segments(const char *hash_method, const uint64_t *dev_seg_addr,
@@ -714,13 +709,22 @@ int mchecksum_gpu_checksum_segments(const char *hash_method, const uint64_t *dev
     a.P = (const uint64_t *)dev_work;
     a.C = (const uint64_t *)dev_work + (nseg + 1);
     a.ragged = (const unsigned long long *)dev_work + 2 * (nseg + 1);
+    const uint64_t nb = (nseg + kScanBlk - 1) / kScanBlk;
+    uint64_t *tot = (uint64_t *)dev_work + 2 * (nseg + 1) + 2;
+    a.obj = tot + 3 * nb;
+    a.map = reinterpret_cast<const uint32_t *>((const uint64_t *)dev_work + seg_words(nseg));
+    // only the CRC-64 queue pass reads the map; MCHECKSUM_GPU_SEG_MAP_CAP caps
+    // the part of it used (tests: 0 forces the search over C)
+    a.map_cap = width == 64 && MCK_SEG_QUEUE ? seg_map_cap(nseg) : 0;
+    if (const char *env = getenv("MCHECKSUM_GPU_SEG_MAP_CAP")) {
+        const uint64_t v = strtoull(env, nullptr, 10);
+        a.map_cap = v < a.map_cap ? v : a.map_cap;
+    }
     a.out = dev_out;
     a.pack = pack;
     a.shift = shift;
     a.err_word = error_word();
-    if (MCK_SEG_QUEUE) a.queue = queue_slot(c, stream);
-    const uint64_t nb = (nseg + kScanBlk - 1) / kScanBlk;
-    uint64_t *tot = (uint64_t *)dev_work + 2 * (nseg + 1) + 2;
+    if (MCK_SEG_QUEUE && width == 64) a.queue = queue_slot(c, stream);
     const uint64_t out_words = (uint64_t)nobj * (uint64_t)(width / 32);
     // at least one block per scan block, and enough to zero the output quickly
     uint64_t zgrid = (out_words + kScanThreads - 1) / kScanThreads;
@@ -731,7 +735,9 @@ int mchecksum_gpu_checksum_segments(const char *hash_method, const uint64_t *dev
     hipLaunchKernelGGL(seg_scan_top, dim3(1), dim3(kScanThreads), 0, s, tot, nb, (uint64_t)nseg, (uint64_t *)a.P,
                        (uint64_t *)a.C, (unsigned long long *)a.ragged);
     if (nb) hipLaunchKernelGGL(seg_scan_down, dim3((unsigned)nb), dim3(kScanThreads), 0, s, dev_seg_len, (uint64_t)nseg,
-                               tot, (uint64_t *)a.P, (uint64_t *)a.C);
+                               tot, (uint64_t *)a.P, (uint64_t *)a.C, dev_obj_first, (uint64_t)nobj,
+                               width == 64 && MCK_SEG_QUEUE ? (uint64_t *)a.obj : nullptr, (uint32_t *)a.map,
+                               a.map_cap);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_err(e, "segment scan launch");
     if (width == 32) {

@@ -81,7 +81,7 @@ def main():
             slots = segment_slots(seed, count * 4)
             seg = G.SegmentBatch([data[int(q) * slen:(int(q) + 1) * slen] for q in slots],
                                  np.arange(0, count * 4 + 1, 4))
-            seg.work = torch.empty(seg.work.numel() + 64, dtype=torch.int64, device="cuda")  # room for any variant
+            seg.work = torch.empty(2 * seg.work.numel() + (1 << 17), dtype=torch.int64, device="cuda")  # room for any variant
             ref = seg.checksum(method)
         elif length is None:
             from mercury_amd.workload import varlen_offsets
