@@ -16,7 +16,7 @@ TICK_US = 0.01  # 100 MHz
 
 
 def main():
-    lib = load(os.path.join(ROOT, "build", "variants", "libmchecksum_trace.so"))
+    lib = load(os.path.join(ROOT, "build", "variants", os.environ.get("TRACE_LIB", "libmchecksum_trace.so")))
     lib.mck_debug_trace_read.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
     lib.mck_debug_qwave_read.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
     out = {}
@@ -81,7 +81,7 @@ def main():
         out[cfg] = med
         del data
         torch.cuda.empty_cache()
-    json.dump(out, open(os.path.join(ROOT, "gpurun_out", "tail_trace.json"), "w"), indent=1)
+    json.dump(out, open(os.path.join(ROOT, "gpurun_out", os.environ.get("TRACE_OUT", "tail_trace.json")), "w"), indent=1)
 
 
 if __name__ == "__main__":
