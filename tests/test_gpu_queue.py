@@ -1,6 +1,6 @@
 """Stress the batch kernels' dynamic work queue: many launches of random
-shapes (fixed and offsets batches, both methods, every lanes-per-payload
-width, both load policies) on the throughput layout, each checked bit for bit against the CPU
+shapes (fixed, offsets and scatter-gather batches, both methods, every
+lanes-per-payload width, both load policies) on the throughput layout, each checked bit for bit against the CPU
 oracle, with a host watchdog (a launch not done after 20 s ends the process
 with exit 3 instead of waiting on a wedged GPU).  Ends with the device's
 queue fault count (must be 0)."""
@@ -40,7 +40,24 @@ def test_dynamic_queue_random_shapes(gpu, oracle_mod, n_iter, monkeypatch):
     t0 = time.time()
     for it in range(n_iter):
         method = ("crc32c", "crc64")[it % 2]
-        if rng.random() < 0.5:
+        r = rng.random()
+        if r < 0.2:
+            # scatter-gather objects: the CRC-64 aligned chunk pass takes the
+            # queue (chunk -> segment map), interleaved on the stream's slot
+            # with the fixed and offsets launches
+            nobj = int(rng.choice([1, 5, 40, 300]))
+            seg_lens = rng.choice([0, 64, 1024, 4096, 262144, 300000, 1 << 20], size=3 * nobj)
+            starts = [int(rng.integers(0, (64 << 20) - int(n) - 64)) // 16 * 16 + int(rng.choice([0, 0, 0, 5]))
+                      for n in seg_lens]
+            first = np.arange(0, 3 * nobj + 1, 3)
+            batch = G.SegmentBatch([dev[a:a + int(n)] for a, n in zip(starts, seg_lens)], first)
+            got = batch.checksum(method)
+            _wait(torch, (it, method, "segments", nobj))
+            want = np.array([O.crc(method, np.concatenate([host[starts[3 * j + q]:starts[3 * j + q] + int(seg_lens[3 * j + q])]
+                                                            for q in range(3)]))
+                             for j in range(nobj)], dtype=np.uint64)
+            tag = ("segments", nobj)
+        elif r < 0.6:
             length = int(rng.choice([0, 1, 16, 1000, 4096, 4100, 16384, 65536, 100003]))
             stride = length + int(rng.choice([0, 0, 16, 3]))
             maxc = max(1, (64 << 20) // max(stride, 1) - 1)
