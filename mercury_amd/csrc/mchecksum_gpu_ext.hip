@@ -71,12 +71,13 @@ struct SegArgs {
     uint32_t *err_word;
 };
 
-// Exclusive prefix sums of segment bytes (P) and chunk counts (C) in three
-// short launches over blocks of kScanBlk segments (one workgroup streams only
+// Exclusive prefix sums of segment bytes (P) and chunk counts (C) in short
+// launches over blocks of kScanBlk segments (one workgroup streams only
 // ~20 GB/s, so a single-workgroup scan of 32768 segments took 48 us):
 // reduce (block totals; also zeroes the output the chunk passes XOR into),
 // top (exclusive scan of the block totals, one workgroup) and down (block-local
-// scan + block offset).  The totals also count segments whose chunks cannot
+// scan + block offset); up to 1 Mi segments, down does top's work itself
+// (two launches).  The totals also count segments whose chunks cannot
 // all take the aligned loop (start not 16-B aligned or length not a multiple
 // of 1 KiB): the CRC-64 ragged pass returns at once when there are none.
 constexpr uint32_t kScanThreads = 256, kScanPer = 4, kScanBlk = kScanThreads * kScanPer;
@@ -183,10 +184,42 @@ __global__ __launch_bounds__(kScanThreads) void seg_scan_top(uint64_t *tot, uint
 
 constexpr uint64_t kNoObj = ~0ull;
 
+// Block offset pass.  FUSED (lists of at most kScanFusedBlocks blocks): the
+// top pass is folded in -- each block sums the raw totals of the blocks before
+// it (a few hundred words at most) and the last block writes the grand totals
+// and the ragged flag -- so the scan takes two launches instead of three.
+constexpr uint64_t kScanFusedBlocks = 1024;
+
+template <bool FUSED>
 __global__ __launch_bounds__(kScanThreads) void seg_scan_down(const uint64_t *len, uint64_t nseg, const uint64_t *tot,
-                                                              uint64_t *P, uint64_t *C, const uint64_t *first,
+                                                              uint64_t nb, uint64_t *P, uint64_t *C,
+                                                              unsigned long long *ragged, const uint64_t *first,
                                                               uint64_t nobj, uint64_t *obj, uint32_t *map,
                                                               uint64_t map_cap) {
+    uint64_t off_p = 0, off_c = 0;
+    uint32_t rag_all = 0;
+    if constexpr (FUSED) {
+        uint64_t sp = 0, sc = 0, sr = 0;
+        for (uint64_t k = threadIdx.x; k < nb; k += kScanThreads) {
+            if (k < blockIdx.x) {
+                sp += tot[3 * k];
+                sc += tot[3 * k + 1];
+            }
+            sr |= tot[3 * k + 2];
+        }
+        block_scan2(sp, sc, &off_p, &off_c);  // block sums of the preceding totals
+        __shared__ uint32_t r;
+        if (threadIdx.x == 0) r = 0;
+        __syncthreads();
+        if (__any(sr != 0) && (threadIdx.x & 63u) == 0) atomicOr(&r, 1u);
+        __syncthreads();
+        rag_all = r;
+    } else {
+        (void)nb;
+        (void)ragged;
+        off_p = tot[3 * blockIdx.x];
+        off_c = tot[3 * blockIdx.x + 1];
+    }
     uint64_t l[kScanPer], p = 0, c = 0;
 #pragma unroll
     for (uint32_t e = 0; e < kScanPer; e++) {
@@ -198,7 +231,12 @@ __global__ __launch_bounds__(kScanThreads) void seg_scan_down(const uint64_t *le
     const uint64_t p0 = p, c0 = c;
     uint64_t tp, tc;
     block_scan2(p, c, &tp, &tc);
-    uint64_t ep = tot[3 * blockIdx.x] + p - p0, ec = tot[3 * blockIdx.x + 1] + c - c0;
+    if (FUSED && blockIdx.x + 1 == nb && threadIdx.x == 0) {
+        P[nseg] = off_p + tp;
+        C[nseg] = off_c + tc;
+        *ragged = rag_all;
+    }
+    uint64_t ep = off_p + p - p0, ec = off_c + c - c0;
     const uint64_t f0 = first[0], f1 = first[nobj];
 #pragma unroll
     for (uint32_t e = 0; e < kScanPer; e++) {
@@ -732,12 +770,22 @@ int mchecksum_gpu_checksum_segments(const char *hash_method, const uint64_t *dev
     const unsigned rgrid = (unsigned)(nb > zgrid ? nb : zgrid > 0 ? zgrid : 1);
     hipLaunchKernelGGL(seg_scan_reduce, dim3(rgrid), dim3(kScanThreads), 0, s, dev_seg_len, dev_seg_addr,
                        (uint64_t)nseg, nb, tot, (uint32_t *)dev_out, out_words);
-    hipLaunchKernelGGL(seg_scan_top, dim3(1), dim3(kScanThreads), 0, s, tot, nb, (uint64_t)nseg, (uint64_t *)a.P,
-                       (uint64_t *)a.C, (unsigned long long *)a.ragged);
-    if (nb) hipLaunchKernelGGL(seg_scan_down, dim3((unsigned)nb), dim3(kScanThreads), 0, s, dev_seg_len, (uint64_t)nseg,
-                               tot, (uint64_t *)a.P, (uint64_t *)a.C, dev_obj_first, (uint64_t)nobj,
-                               width == 64 && MCK_SEG_QUEUE ? (uint64_t *)a.obj : nullptr, (uint32_t *)a.map,
-                               a.map_cap);
+    uint64_t *obj_w = width == 64 && MCK_SEG_QUEUE ? (uint64_t *)a.obj : nullptr;
+    const char *scan3 = getenv("MCHECKSUM_GPU_SEG_SCAN3");  // tests: force the three-launch scan
+    if (nb >= 1 && nb <= kScanFusedBlocks && !(scan3 && scan3[0] == '1')) {
+        hipLaunchKernelGGL(seg_scan_down<true>, dim3((unsigned)nb), dim3(kScanThreads), 0, s, dev_seg_len,
+                           (uint64_t)nseg, (const uint64_t *)tot, nb, (uint64_t *)a.P, (uint64_t *)a.C,
+                           (unsigned long long *)a.ragged, dev_obj_first, (uint64_t)nobj, obj_w, (uint32_t *)a.map,
+                           a.map_cap);
+    } else {
+        hipLaunchKernelGGL(seg_scan_top, dim3(1), dim3(kScanThreads), 0, s, tot, nb, (uint64_t)nseg, (uint64_t *)a.P,
+                           (uint64_t *)a.C, (unsigned long long *)a.ragged);
+        if (nb)
+            hipLaunchKernelGGL(seg_scan_down<false>, dim3((unsigned)nb), dim3(kScanThreads), 0, s, dev_seg_len,
+                               (uint64_t)nseg, (const uint64_t *)tot, nb, (uint64_t *)a.P, (uint64_t *)a.C,
+                               (unsigned long long *)a.ragged, dev_obj_first, (uint64_t)nobj, obj_w,
+                               (uint32_t *)a.map, a.map_cap);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_err(e, "segment scan launch");
     if (width == 32) {

@@ -224,10 +224,14 @@ def test_core_headers_reject_wide_methods(gpu):
 
 
 @pytest.mark.parametrize("method", ["crc32c", "crc64"])
-def test_segments_long_lists_multi_block_scan(gpu, buf, oracle_mod, method):
-    """300000 short segments (the prefix scan runs in 293 blocks, so its
-    block-offset pass takes two tiles) and an all-aligned list (every chunk on
-    the aligned pass: the CRC-64 ragged pass returns at once)."""
+@pytest.mark.parametrize("scan3", [False, True])
+def test_segments_long_lists_multi_block_scan(gpu, buf, oracle_mod, method, scan3, monkeypatch):
+    """300000 short segments (the prefix scan runs in 293 blocks: the fused
+    block-offset pass sums up to 292 preceding totals; scan3 forces the
+    three-launch scan, whose top pass takes two tiles) and an all-aligned list
+    (every chunk on the aligned pass: the CRC-64 ragged pass returns at once)."""
+    if scan3:
+        monkeypatch.setenv("MCHECKSUM_GPU_SEG_SCAN3", "1")
     host = _host(buf)
     rng = np.random.default_rng(91)
     lens = rng.integers(0, 65, 300000)
