@@ -16,8 +16,9 @@
  *
  * Implementation: reflected models run slicing-by-8 on the reflected
  * register (tables built once per model under pthread_once), crc32c uses the
- * SSE4.2 crc32 instruction when the CPU has it; MSB-first models run a byte
- * table.  No global mutable state after table construction, so distinct
+ * SSE4.2 crc32 instruction when the CPU has it -- and for updates of 1 KiB
+ * and more an AVX-512 VPCLMULQDQ carry-less-multiply fold reduced by the
+ * crc32 instruction; MSB-first models run a byte table.  No global mutable state after table construction, so distinct
  * objects are safe to use from different threads concurrently.
  */
 #define _GNU_SOURCE
@@ -116,20 +117,123 @@ static const uint64_t (*tables_for(int idx))[256]
 /* ---------------------------------------------------------------------- */
 
 #if defined(__x86_64__)
+#include <immintrin.h>
+
 static pthread_once_t g_hw_once = PTHREAD_ONCE_INIT;
 static int g_hw_crc32c;
+/* carry-less-multiply fold constants for moving a 16-byte block D bits
+ * forward: { rev32(x^(D+63) mod P) << 32, rev32(x^(D-1) mod P) << 32 } (one
+ * power less than the move because the product of two reflected operands comes
+ * out one bit low), for D = 2048, 512 and 128 */
+static uint64_t g_k512[2], g_k128[2], g_k2048[2];
+static int g_hw_vclmul;
+
+static uint32_t
+xpow_mod_crc32c(unsigned n)
+{
+    uint64_t r = 1;
+    while (n--) {
+        r <<= 1;
+        if (r >> 32)
+            r ^= 0x11EDC6F41ULL; /* x^32 + Castagnoli polynomial */
+    }
+    return (uint32_t) r;
+}
+
+static uint64_t
+fold_const(unsigned n)
+{
+    return mck_reflect(xpow_mod_crc32c(n), 32) << 32;
+}
 
 static void
 detect_hw(void)
 {
     const char *env = getenv("MCHECKSUM_DISABLE_SSE42");
+    const char *envc = getenv("MCHECKSUM_DISABLE_CLMUL");
     __builtin_cpu_init();
     g_hw_crc32c = __builtin_cpu_supports("sse4.2") && !(env && env[0] == '1');
+    g_k512[0] = fold_const(512 + 63);
+    g_k512[1] = fold_const(512 - 1);
+    g_k128[0] = fold_const(128 + 63);
+    g_k128[1] = fold_const(128 - 1);
+    g_k2048[0] = fold_const(2048 + 63);
+    g_k2048[1] = fold_const(2048 - 1);
+    g_hw_vclmul = g_hw_crc32c && __builtin_cpu_supports("pclmul") && __builtin_cpu_supports("avx512f") &&
+                  __builtin_cpu_supports("vpclmulqdq") && !(envc && envc[0] == '1');
 }
+
+__attribute__((target("sse4.2,pclmul"))) static inline __m128i
+clmul_fold(__m128i a, __m128i k)
+{
+    /* a.lo is the higher-degree half of the block (reflected), k = {k1, k2} */
+    return _mm_xor_si128(_mm_clmulepi64_si128(a, k, 0x00), _mm_clmulepi64_si128(a, k, 0x11));
+}
+
+/* Carry-less-multiply fold (AVX-512 VPCLMULQDQ), n >= 256: four 64-byte
+ * registers of four 16-byte lanes fold 256 bytes per step (D = 2048), then
+ * into one register (D = 512) and its four lanes into one block (D = 128)
+ * congruent to the data so far (mod P, same bit alignment); the crc32
+ * instruction reduces that block and the tail.  The incoming register is
+ * XORed into the first 4 bytes (a reflected CRC's register is the same as
+ * those bytes' XOR).  On the EPYC 9575F host: C1 (4 KiB updates) 52 GiB/s vs
+ * 27 GiB/s for the three-stream crc32 loop; a 16-byte PCLMULQDQ fold measured
+ * 17 GiB/s there, so CPUs without AVX-512 VPCLMULQDQ keep the crc32 loop. */
+__attribute__((target("avx512f,vpclmulqdq"))) static inline __m512i
+vclmul_fold_xor(__m512i a, __m512i k, __m512i b)
+{
+    return _mm512_ternarylogic_epi64(_mm512_clmulepi64_epi128(a, k, 0x00), _mm512_clmulepi64_epi128(a, k, 0x11), b,
+                                     0x96);
+}
+
+__attribute__((target("avx512f,vpclmulqdq,sse4.2,pclmul"))) static uint64_t
+crc32c_vclmul(uint64_t c, const uint8_t *d, size_t n)
+{
+    const __m512i k2048 = _mm512_broadcast_i32x4(_mm_set_epi64x((long long) g_k2048[1], (long long) g_k2048[0]));
+    const __m512i k512 = _mm512_broadcast_i32x4(_mm_set_epi64x((long long) g_k512[1], (long long) g_k512[0]));
+    const __m128i k128 = _mm_set_epi64x((long long) g_k128[1], (long long) g_k128[0]);
+    __m512i z0 = _mm512_xor_si512(_mm512_loadu_si512(d), _mm512_castsi128_si512(_mm_cvtsi32_si128((int) (uint32_t) c)));
+    __m512i z1 = _mm512_loadu_si512(d + 64), z2 = _mm512_loadu_si512(d + 128), z3 = _mm512_loadu_si512(d + 192);
+    d += 256;
+    n -= 256;
+    while (n >= 256) {
+        z0 = vclmul_fold_xor(z0, k2048, _mm512_loadu_si512(d));
+        z1 = vclmul_fold_xor(z1, k2048, _mm512_loadu_si512(d + 64));
+        z2 = vclmul_fold_xor(z2, k2048, _mm512_loadu_si512(d + 128));
+        z3 = vclmul_fold_xor(z3, k2048, _mm512_loadu_si512(d + 192));
+        d += 256;
+        n -= 256;
+    }
+    z1 = vclmul_fold_xor(z0, k512, z1);
+    z2 = vclmul_fold_xor(z1, k512, z2);
+    z3 = vclmul_fold_xor(z2, k512, z3);
+    __m128i a = _mm512_castsi512_si128(z3);
+    a = _mm_xor_si128(clmul_fold(a, k128), _mm512_extracti32x4_epi32(z3, 1));
+    a = _mm_xor_si128(clmul_fold(a, k128), _mm512_extracti32x4_epi32(z3, 2));
+    a = _mm_xor_si128(clmul_fold(a, k128), _mm512_extracti32x4_epi32(z3, 3));
+    uint64_t r = _mm_crc32_u64(0, (uint64_t) _mm_cvtsi128_si64(a));
+    r = _mm_crc32_u64(r, (uint64_t) _mm_extract_epi64(a, 1));
+    while (n >= 8) {
+        uint64_t w;
+        memcpy(&w, d, 8);
+        r = _mm_crc32_u64(r, w);
+        d += 8;
+        n -= 8;
+    }
+    while (n--)
+        r = _mm_crc32_u8((uint32_t) r, *d++);
+    return r;
+}
+
+/* Updates of at least this many bytes take the fold (below it the
+ * three-stream crc32 loop wins: the fold's setup and reduction are fixed). */
+#define MCK_CLMUL_MIN 1024
 
 __attribute__((target("sse4.2"))) static uint64_t
 crc32c_hw(uint64_t c, const uint8_t *d, size_t n)
 {
+    if (n >= MCK_CLMUL_MIN && g_hw_vclmul)
+        return crc32c_vclmul(c, d, n);
     while (n && ((uintptr_t) d & 7)) {
         c = __builtin_ia32_crc32qi((uint32_t) c, *d++);
         n--;

@@ -193,27 +193,37 @@ def test_streaming_matches_oracle_random(product_lib, oracle_mod, method):
         assert c.get() == oracle_mod.crc(method, d), (method, off, n, cuts)
 
 
+_PATH_LENS = (0, 1, 767, 768, 769, 1023, 1024, 1025, 1536, 2304, 4096, 5000, 9999, 65536 + 13, 262144 + 255)
+
+
 def test_sse42_and_software_paths_agree(product_lib, oracle_mod):
-    """The SSE4.2 path (3-way interleave + shift combine) and the slicing path
-    (forced with MCHECKSUM_DISABLE_SSE42=1, read once per process) agree."""
+    """Every CPU CRC-32C path agrees with the oracle's bitwise model: the
+    AVX-512 VPCLMULQDQ fold (default where the CPU has it), the SSE4.2 3-way
+    interleave + shift combine (MCHECKSUM_DISABLE_CLMUL=1) and the slicing path
+    (MCHECKSUM_DISABLE_SSE42=1) -- each knob is read once per process, so each
+    path runs in a subprocess, on lengths around every path's thresholds, at
+    an odd start offset, whole and as a 3-way split update."""
     import subprocess
     import sys
     code = ("import sys; sys.path.insert(0, %r)\n"
-            "from mercury_amd import checksum\n"
+            "from mercury_amd import checksum, Checksum\n"
             "from oracle import oracle as O\n"
-            "buf = O.splitmix_bytes(10000, 0x55)\n"
-            "print(','.join(str(checksum('crc32c', buf[3:3+n].tobytes())) for n in "
-            "(0, 1, 767, 768, 769, 1536, 2304, 5000, 9999)))\n") % ROOT
+            "buf = O.splitmix_bytes(300000, 0x55)\n"
+            "out = []\n"
+            "for n in %r:\n"
+            "    d = buf[3:3 + n].tobytes()\n"
+            "    c = Checksum('crc32c'); c.update(d[:n // 3]); c.update(d[n // 3:n - 7]); c.update(d[n - 7:] if n >= 7 else b'')\n"
+            "    out.append('%%d/%%d' %% (checksum('crc32c', d), c.get() if n >= 7 else checksum('crc32c', d)))\n"
+            "print(','.join(out))\n") % (ROOT, _PATH_LENS)
     outs = []
-    for env in ({}, {"MCHECKSUM_DISABLE_SSE42": "1"}):
+    for env in ({}, {"MCHECKSUM_DISABLE_CLMUL": "1"}, {"MCHECKSUM_DISABLE_SSE42": "1"}):
         r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
                            env={**os.environ, **env})
         assert r.returncode == 0, r.stderr
         outs.append(r.stdout.strip())
-    buf = oracle_mod.splitmix_bytes(10000, 0x55)
-    want = ",".join(str(oracle_mod.crc("crc32c", buf[3:3 + n], "bitwise"))
-                    for n in (0, 1, 767, 768, 769, 1536, 2304, 5000, 9999))
-    assert outs[0] == outs[1] == want
+    buf = oracle_mod.splitmix_bytes(300000, 0x55)
+    want = ",".join("%d/%d" % ((oracle_mod.crc("crc32c", buf[3:3 + n], "bitwise"),) * 2) for n in _PATH_LENS)
+    assert outs == [want] * 3
 
 
 def test_stream_split_fixture(product_lib):
