@@ -175,7 +175,8 @@ def test_variant_environment_override(product_lib, monkeypatch):
     assert checksum("crc64", b"123456789") == int(cat["crc64-xz"]["check"], 16)
 
 
-@pytest.mark.parametrize("method", ["crc32c", "crc64", "crc16", "crc32", "crc64-ecma182", "crc16-arc"])
+@pytest.mark.parametrize("method", ["crc32c", "crc64", "crc16", "crc32", "crc64-ecma182", "crc16-arc", "crc64-go-iso",
+                                    "crc64-jones", "crc16-kermit"])
 def test_streaming_matches_oracle_random(product_lib, oracle_mod, method):
     from mercury_amd import Checksum
     buf = oracle_mod.splitmix_bytes(200000, 0xABC)
@@ -197,9 +198,10 @@ _PATH_LENS = (0, 1, 767, 768, 769, 1023, 1024, 1025, 1536, 2304, 4096, 5000, 999
 
 
 def test_sse42_and_software_paths_agree(product_lib, oracle_mod):
-    """Every CPU CRC-32C path agrees with the oracle's bitwise model: the
-    AVX-512 VPCLMULQDQ fold (default where the CPU has it), the SSE4.2 3-way
-    interleave + shift combine (MCHECKSUM_DISABLE_CLMUL=1) and the slicing path
+    """Every CPU path agrees with the oracle's bitwise model, for crc32c and
+    crc64: the AVX-512 VPCLMULQDQ fold (default where the CPU has it), the
+    SSE4.2 3-way interleave + shift combine / slicing-by-8
+    (MCHECKSUM_DISABLE_CLMUL=1) and the slicing path
     (MCHECKSUM_DISABLE_SSE42=1) -- each knob is read once per process, so each
     path runs in a subprocess, on lengths around every path's thresholds, at
     an odd start offset, whole and as a 3-way split update."""
@@ -210,10 +212,11 @@ def test_sse42_and_software_paths_agree(product_lib, oracle_mod):
             "from oracle import oracle as O\n"
             "buf = O.splitmix_bytes(300000, 0x55)\n"
             "out = []\n"
-            "for n in %r:\n"
+            "for m in ('crc32c', 'crc64'):\n"
+            "  for n in %r:\n"
             "    d = buf[3:3 + n].tobytes()\n"
-            "    c = Checksum('crc32c'); c.update(d[:n // 3]); c.update(d[n // 3:n - 7]); c.update(d[n - 7:] if n >= 7 else b'')\n"
-            "    out.append('%%d/%%d' %% (checksum('crc32c', d), c.get() if n >= 7 else checksum('crc32c', d)))\n"
+            "    c = Checksum(m); c.update(d[:n // 3]); c.update(d[n // 3:n - 7]); c.update(d[n - 7:] if n >= 7 else b'')\n"
+            "    out.append('%%d/%%d' %% (checksum(m, d), c.get() if n >= 7 else checksum(m, d)))\n"
             "print(','.join(out))\n") % (ROOT, _PATH_LENS)
     outs = []
     for env in ({}, {"MCHECKSUM_DISABLE_CLMUL": "1"}, {"MCHECKSUM_DISABLE_SSE42": "1"}):
@@ -222,7 +225,8 @@ def test_sse42_and_software_paths_agree(product_lib, oracle_mod):
         assert r.returncode == 0, r.stderr
         outs.append(r.stdout.strip())
     buf = oracle_mod.splitmix_bytes(300000, 0x55)
-    want = ",".join("%d/%d" % ((oracle_mod.crc("crc32c", buf[3:3 + n], "bitwise"),) * 2) for n in _PATH_LENS)
+    want = ",".join("%d/%d" % ((oracle_mod.crc(m, buf[3:3 + n], "bitwise"),) * 2)
+                    for m in ("crc32c", "crc64") for n in _PATH_LENS)
     assert outs == [want] * 3
 
 
