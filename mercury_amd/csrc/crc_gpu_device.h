@@ -68,8 +68,8 @@ struct Tab32 {
 // MCK_CRC64_P6=1 instead looks a 64-bit word up in 12 tables (pack f5/f6):
 // bits 3..7 of each byte index a 32-entry table at 8-B stride -- one 256-B
 // row, entry v on bank pair v, conflict-free without copies, address =
-// (byte & 0xF8) --, and bits 0..2 of bytes 2i and 2i+1, gathered into one
-// 6-bit index by a shift + bit-select per 32-bit half, a 64-entry table
+// (byte & 0xF8) --, and bits 0..2 of bytes i and i+4, gathered into one
+// 6-bit index by one shift + bit-select for all four, a 64-entry table
 // replicated 32x (entry v at v*256 B + lane copy, 16 KiB per table).  Three
 // quarters of the LDS reads of the nibble form; the combine operators then
 // move to global memory so two workgroups per CU still fit.
@@ -1256,20 +1256,24 @@ MCK_SDWA_P6(1)
 MCK_SDWA_P6(2)
 MCK_SDWA_P6(3)
 #undef MCK_SDWA_P6
-// bits 0..2 of each byte of x and bits 0..4 of each byte of (x >> 5): one
-// v_bfi_b32 (mask in an SGPR; VOP3 takes no literal on gfx9).  The C form
-// (x & m) | (y & ~m) compiled to v_and + v_and_or: one VALU op more per
-// 32-bit half on a VALU-bound loop.
+// Byte i of the result: bits 0..2 of byte i of the low half xl and, above
+// them, bits 0..4 of byte i of the high half xh -- the 6-bit index of pair
+// table i (bytes i and i + 4 of the word; sdwa_p6 keeps 6 bits).  One shift
+// and one v_bfi_b32 (mask in an SGPR; VOP3 takes no literal on gfx9) for all
+// four pair indexes: round 1 paired bytes (2i, 2i+1) within a half, which took
+// a shift and a bit-select per half (28 -> 26 VALU ops per 8-byte word on a
+// VALU-bound loop).  The C form (x & m) | (y & ~m) compiled to v_and +
+// v_and_or: one op more.
 #ifndef MCK_BFI64
 #define MCK_BFI64 1
 #endif
-__device__ __forceinline__ uint32_t gather6(uint32_t x) {
+__device__ __forceinline__ uint32_t gather6(uint32_t xl, uint32_t xh) {
 #if MCK_BFI64
     uint32_t r;
-    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(0x07070707u), "v"(x), "v"(x >> 5));
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(0x07070707u), "v"(xl), "v"(xh << 3));
     return r;
 #else
-    return (x & 0x07070707u) | ((x >> 5) & ~0x07070707u);
+    return (xl & 0x07070707u) | ((xh << 3) & ~0x07070707u);
 #endif
 }
 __device__ __forceinline__ uint64_t xor13(const uint64_t *r, uint64_t extra) {
@@ -1279,9 +1283,8 @@ __device__ __forceinline__ uint64_t xor13(const uint64_t *r, uint64_t extra) {
 // Z^(16G)(x) ^ next from the 12 tables f5/f6 (LDS map above).
 __device__ __forceinline__ uint64_t f64x(const uint8_t *lds, uint64_t x, uint64_t next, Lane64 &ln) {
     const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
-    // byte 2i' of t: bits 0..2 of bytes 2i', 2i'+1 of the half (bit-select)
-    const uint32_t tl = gather6(xl);
-    const uint32_t th = gather6(xh);
+    // byte i of t: bits 0..2 of bytes i and i + 4 of the word (bit-select)
+    const uint32_t t = gather6(xl, xh);
     uint64_t r[12];
     r[0] = lds64(lds, sdwa_f8_0(xl) + kL64P5 + 0 * 256);
     r[1] = lds64(lds, sdwa_f8_1(xl) + kL64P5 + 1 * 256);
@@ -1291,13 +1294,13 @@ __device__ __forceinline__ uint64_t f64x(const uint8_t *lds, uint64_t x, uint64_
     r[5] = lds64(lds, sdwa_f8_1(xh) + kL64P5 + 5 * 256);
     r[6] = lds64(lds, sdwa_f8_2(xh) + kL64P5 + 6 * 256);
     r[7] = lds64(lds, sdwa_f8_3(xh) + kL64P5 + 7 * 256);
-    sdwa_p6_0(ln.al[0], tl);
+    sdwa_p6_0(ln.al[0], t);
     r[8] = lds64(lds, ln.al[0] + kL64P6 + 0 * 16384);
-    sdwa_p6_2(ln.al[1], tl);
+    sdwa_p6_1(ln.al[1], t);
     r[9] = lds64(lds, ln.al[1] + kL64P6 + 1 * 16384);
-    sdwa_p6_0(ln.al[2], th);
+    sdwa_p6_2(ln.al[2], t);
     r[10] = lds64(lds, ln.al[2] + kL64P6 + 2 * 16384);
-    sdwa_p6_2(ln.al[3], th);
+    sdwa_p6_3(ln.al[3], t);
     r[11] = lds64(lds, ln.al[3] + kL64P6 + 3 * 16384);
     return xor13(r, next);
 }

@@ -55,9 +55,9 @@ typedef struct {
     uint32_t nops;
     /* Fewer-lookup form of the same step fold F = Z^(16G) (12 lookups per
      * 64-bit word instead of 16): bits 3..7 of byte j index a 32-entry table,
-     * bits 0..2 of bytes 2i and 2i+1 together a 64-entry table.            */
+     * bits 0..2 of bytes i and i+4 together a 64-entry table.              */
     uint64_t f5[8][32];               /* f5[j][v] = F(v << (8j + 3))         */
-    uint64_t f6[4][64];               /* f6[i][v] = F((v&7) << 16i | (v>>3) << (16i+8)) */
+    uint64_t f6[4][64];               /* f6[i][v] = F((v&7) << 8i | (v>>3) << (8i+32)) */
 } crc64_gpu_pack_t;
 
 /* ---- register shifts Z^n for 0 <= n < 2^48 (scatter-gather combine) ----- */

@@ -251,8 +251,8 @@ crc64_gpu_pack_build(const crc_rmodel_t *m, int log2g, crc64_gpu_pack_t *out)
             out->f5[p][v] = crc_op_apply(64, op, (uint64_t) v << (8 * p + 3));
     for (p = 0; p < 4; p++)
         for (v = 0; v < 64; v++)
-            out->f6[p][v] = crc_op_apply(64, op, ((uint64_t) (v & 7) << (16 * p)) |
-                                                     ((uint64_t) (v >> 3) << (16 * p + 8)));
+            out->f6[p][v] = crc_op_apply(64, op, ((uint64_t) (v & 7) << (8 * p)) |
+                                                     ((uint64_t) (v >> 3) << (8 * p + 32)));
     if (fill_nibble_op64(m, -8, out->ops[o++]))
         return -1;
     for (k = 0; k < log2g; k++)

@@ -118,7 +118,7 @@ extern "C" uint64_t emu_crc64(const crc64_gpu_pack_t *pk, const uint8_t *buf, in
                 // the kernels' 12-lookup form (f5 / f6) of the same fold
                 for (int p = 0; p < 8; p++) r6 ^= pk->f5[p][(x >> (8 * p + 3)) & 31];
                 for (int i = 0; i < 4; i++)
-                    r6 ^= pk->f6[i][((x >> (16 * i)) & 7) | (((x >> (16 * i + 8)) & 7) << 3)];
+                    r6 ^= pk->f6[i][((x >> (8 * i)) & 7) | (((x >> (8 * i + 32)) & 7) << 3)];
                 if (r6 != r) {
                     std::fprintf(stderr, "emu_crc64: f5/f6 fold differs from the nibble fold\n");
                     std::abort();
