@@ -119,10 +119,23 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         torch.cuda.set_device(local % torch.cuda.device_count())
-        if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group("gloo")
+        # The communication libraries may print connection notices on file
+        # descriptor 1 (gloo's "[Gloo] Rank 0 is connected to ..."), which
+        # would corrupt the one-JSON-line stdout contract: point fd 1 at
+        # stderr while the group comes up.
+        sys.stdout.flush()
+        saved_fd = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            if args.backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            else:
+                dist.init_process_group("gloo")
+            dist.barrier()  # connections are made by the first collective at the latest
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved_fd, 1)
+            os.close(saved_fd)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
