@@ -219,7 +219,9 @@ class SegmentBatch:
     the bulk-handle shape, HG_Bulk_create's (buf_ptrs, buf_sizes) in device
     memory.  The segment table and the scan workspace stay on the device, so
     `checksum` is one C-ABI call (no host work per launch).  Keep the segment
-    tensors alive while the batch is in use."""
+    tensors alive while the batch is in use.  Calls share the one workspace,
+    so a call on another stream than the previous call's first waits for it
+    (the C ABI requires a workspace per concurrent call)."""
 
     def __init__(self, segments, obj_first=None, device=None):
         import numpy as np
@@ -245,6 +247,7 @@ class SegmentBatch:
                                                      np.asarray(lens, dtype=np.int64), first])).to(self.device)
         self.work = torch.empty((_lib().mchecksum_gpu_segments_work_size(self.nseg) + 7) // 8, dtype=torch.int64,
                                 device=self.device)
+        self._last = None  # (stream handle, event after the last call)
 
     def checksum(self, method: str, out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
         if out is None:
@@ -255,9 +258,19 @@ class SegmentBatch:
             raise GpuChecksumError(f"out must be on {self.device}")
         base, n = self.meta.data_ptr(), self.nseg
         with torch.cuda.device(self.device):
+            h = _stream_handle(stream, self.device)
+            # (graph capture: replays are ordered by the graph's user; no events)
+            track = not torch.cuda.is_current_stream_capturing()
+            s = (torch.cuda.ExternalStream(h) if h else torch.cuda.default_stream(self.device)) if track else None
+            if track and self._last is not None and self._last[0] != h:
+                s.wait_event(self._last[1])  # the workspace is still the previous call's
             rc = _lib().mchecksum_gpu_checksum_segments(method.encode(), base, base + 8 * n, n, base + 16 * n,
                                                         self.nobj, self.work.data_ptr(), self.work.numel() * 8,
-                                                        out.data_ptr(), _stream_handle(stream, self.device))
+                                                        out.data_ptr(), h)
+            if rc == 0 and track:
+                ev = torch.cuda.Event()
+                ev.record(s)
+                self._last = (h, ev)
         if rc != 0:
             _err(rc, "mchecksum_gpu_checksum_segments")
         return out

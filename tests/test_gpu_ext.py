@@ -262,3 +262,26 @@ def test_segments_large_batch_non_temporal(gpu, buf, oracle_mod, method):
     got = gpu.as_unsigned(gpu.checksum_segments(method, [buf[o:o + n] for o, n in segs], first)).tolist()
     for j in (0, 1, 17, 80, 159):
         assert got[j] == _want(oracle_mod, method, host, segs[first[j]:first[j + 1]], [0, 4])[0], j
+
+
+def test_segment_batch_calls_on_two_streams(gpu, buf, oracle_mod):
+    """One SegmentBatch used on two streams back to back: the calls share its
+    workspace, so the second waits for the first (gpu.SegmentBatch) and both
+    results equal the oracle."""
+    import torch
+    host = _host(buf)
+    rng = np.random.default_rng(404)
+    segs, first = _objects(rng, buf.numel() - 64, 60)
+    batch = gpu.SegmentBatch([buf[o:o + n] for o, n in segs], first)
+    want = _want(oracle_mod, "crc64", host, segs, first)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    outs = []
+    for rep in range(20):
+        o1 = torch.zeros(len(first) - 1, dtype=torch.int64, device="cuda")
+        o2 = torch.zeros(len(first) - 1, dtype=torch.int64, device="cuda")
+        batch.checksum("crc64", out=o1, stream=s1)
+        batch.checksum("crc64", out=o2, stream=s2)
+        outs += [o1, o2]
+    torch.cuda.synchronize()
+    for o in outs:
+        assert gpu.as_unsigned(o).tolist() == want
