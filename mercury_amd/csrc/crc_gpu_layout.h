@@ -75,15 +75,23 @@ typedef struct {
 extern "C" {
 #endif
 
-/* Reflected CRC model as the kernels see it. */
+/* Reflected CRC model as the kernels see it.  msb = 1: an MSB-first model
+ * (refin = refout = false), run as the reflected model of the same polynomial
+ * over bit-reversed bytes -- with every operator conjugated by R, the bit
+ * reversal within each byte of the register (R o Z o R), so the kernels XOR
+ * the data bytes in unchanged; rinit and xorout are then given in that R
+ * domain, and the kernel's output v is the CRC byte-swapped (reflect_W(R(v))
+ * = bswap(v)): the host swaps the outputs after the launch. */
 typedef struct {
     int width;        /* 32 or 64 */
     uint64_t rpoly;   /* reflected polynomial */
     uint64_t rinit;   /* initial register in reflected form */
     uint64_t xorout;
+    int msb;
 } crc_rmodel_t;
 
 /* Host generators (crc_tables.c). Return 0 on success. */
+uint64_t crc_rev_bytes(int w, uint64_t v);
 int crc32_gpu_pack_build(const crc_rmodel_t *m, int log2g, crc32_gpu_pack_t *out);
 int crc64_gpu_pack_build(const crc_rmodel_t *m, int log2g, crc64_gpu_pack_t *out);
 int crc32_shift_pack_build(const crc_rmodel_t *m, crc32_shift_pack_t *out);

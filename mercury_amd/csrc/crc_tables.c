@@ -28,13 +28,28 @@ zero_byte(const crc_rmodel_t *m, uint64_t r)
     return r & wmask(m->width);
 }
 
+/* Bit reversal within each byte of a w-bit value (the R of crc_rmodel_t). */
+uint64_t
+crc_rev_bytes(int w, uint64_t v)
+{
+    uint64_t r = 0;
+    int b, k;
+
+    for (b = 0; b < w / 8; b++)
+        for (k = 0; k < 8; k++)
+            if ((v >> (8 * b + k)) & 1)
+                r |= 1ULL << (8 * b + 7 - k);
+    return r;
+}
+
 void
 crc_op_zero_byte(const crc_rmodel_t *m, uint64_t *col)
 {
     int i;
 
     for (i = 0; i < m->width; i++)
-        col[i] = zero_byte(m, 1ULL << i);
+        col[i] = m->msb ? crc_rev_bytes(m->width, zero_byte(m, 1ULL << ((i & ~7) | (7 - (i & 7)))))
+                        : zero_byte(m, 1ULL << i);
 }
 
 void

@@ -39,8 +39,14 @@ extern std::mutex g_mu;
 // Record a formatted error for mchecksum_gpu_last_error(); returns rc.
 int set_err(int rc, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
 int hip_err(hipError_t e, const char *what);
-// Method -> model index for GPU batch kernels (reflected 32/64-bit): -1 unknown, -2 no kernel.
+// Method -> model index for GPU batch kernels (32/64-bit): -1 unknown, -2 no kernel.
 int gpu_model(const char *method, int *width);
+// The kernels' form of catalogue model idx (MSB-first models in the byte-
+// reversed register domain, crc_gpu_layout.h), and whether it is MSB-first:
+// then the host byte-swaps the outputs after the launch (swap_outputs).
+crc_rmodel_t gpu_rmodel(int idx);
+bool gpu_msb(int idx);
+int swap_outputs(void *dev_out, uint64_t count, int width, void *stream);
 // Current device's context (caller holds g_mu).
 int device_ctx(DevCtx **out);
 // Model + device context + table pack for lanes-per-payload 2^log2g (takes g_mu).

@@ -68,14 +68,52 @@ int hip_err(hipError_t e, const char *what) {
 std::mutex g_mu;
 DevCtx g_dev[kMaxDev];
 
-// Method -> (model index, width) for GPU-capable (reflected 32/64-bit) models.
+// Method -> (model index, width) for GPU-capable (32/64-bit) models.
 int gpu_model(const char *method, int *width) {
     const int idx = mck_model_index(method);
     if (idx < 0) return -1;
     const mck_model_t &m = mck_models[idx];
-    if (!m.reflected || (m.width != 32 && m.width != 64)) return -2;
+    if (m.width != 32 && m.width != 64) return -2;
     *width = m.width;
     return idx;
+}
+
+bool gpu_msb(int idx) { return !mck_models[idx].reflected; }
+
+// A reflected model as is; an MSB-first model as the reflected model of the
+// same polynomial over bit-reversed bytes, conjugated by R (crc_gpu_layout.h):
+// rinit / xorout reflected, then R-mapped.
+crc_rmodel_t gpu_rmodel(int idx) {
+    const mck_model_t &m = mck_models[idx];
+    crc_rmodel_t rm{};
+    rm.width = m.width;
+    rm.rpoly = mck_reflect(m.poly, m.width);
+    rm.msb = !m.reflected;
+    rm.rinit = rm.msb ? crc_rev_bytes(m.width, mck_reflect(m.init, m.width)) : mck_reflect(m.init, m.width);
+    rm.xorout = rm.msb ? crc_rev_bytes(m.width, mck_reflect(m.xorout, m.width)) : m.xorout;
+    return rm;
+}
+
+__global__ __launch_bounds__(256) void bswap_kernel(void *out, uint64_t n, int width) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        if (width == 64) {
+            unsigned long long *p = reinterpret_cast<unsigned long long *>(out) + i;
+            *p = __builtin_bswap64(*p);
+        } else {
+            uint32_t *p = reinterpret_cast<uint32_t *>(out) + i;
+            *p = __builtin_bswap32(*p);
+        }
+    }
+}
+
+int swap_outputs(void *dev_out, uint64_t count, int width, void *stream) {
+    if (!count) return MCHECKSUM_GPU_OK;
+    uint64_t blocks = (count + 255) / 256;
+    blocks = blocks > 1024 ? 1024 : blocks;
+    hipLaunchKernelGGL(bswap_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, dev_out, count, width);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_err(e, "output byte swap");
+    return MCHECKSUM_GPU_OK;
 }
 
 int device_ctx(DevCtx **out) {
@@ -110,11 +148,7 @@ int get_pack(DevCtx *c, int idx, int log2g, const void **pack) {
         return 0;
     }
     const mck_model_t &m = mck_models[idx];
-    crc_rmodel_t rm;
-    rm.width = m.width;
-    rm.rpoly = mck_reflect(m.poly, m.width);
-    rm.rinit = mck_reflect(m.init, m.width);
-    rm.xorout = m.xorout;
+    const crc_rmodel_t rm = gpu_rmodel(idx);
     void *host = nullptr;
     size_t bytes = 0;
     int rc;
@@ -270,7 +304,7 @@ unsigned grid_for(const DevCtx *c, uint64_t waves_needed, const KLaunch &kl) {
 int prologue(const char *method, int log2g, int *width, DevCtx **c, const void **pack) {
     int idx = gpu_model(method, width);
     if (idx == -1) return set_err(MCHECKSUM_GPU_EMETHOD, "unknown hash method \"%s\"", method ? method : "(null)");
-    if (idx < 0) return set_err(MCHECKSUM_GPU_EMETHOD, "method \"%s\" has no GPU kernel (reflected 32/64-bit only)", method);
+    if (idx < 0) return set_err(MCHECKSUM_GPU_EMETHOD, "method \"%s\" has no GPU kernel (32/64-bit only)", method);
     std::lock_guard<std::mutex> lk(g_mu);
     int rc = device_ctx(c);
     if (rc) return rc;
@@ -312,6 +346,9 @@ int do_offsets(const char *method, const void *base, const uint64_t *offsets, si
     a.err_word = t_err_word;
     if (msg && width != 32)
         return set_err(MCHECKSUM_GPU_EMETHOD, "message verify carries a 32-bit header hash: crc32c only");
+    const int midx = gpu_model(method, &width);
+    if (verify && gpu_msb(midx))
+        return set_err(MCHECKSUM_GPU_EMETHOD, "verify of MSB-first method \"%s\": checksum and compare instead", method);
     KLaunch k;
     // The offsets table stays on the device, so size the batch by its count:
     // 8192+ payloads of the C4 mix are ~270 MB and up.
@@ -328,7 +365,9 @@ int do_offsets(const char *method, const void *base, const uint64_t *offsets, si
         k = verify ? (nt ? kernel_ptr<64, 6, kOffsets, true, true>() : kernel_ptr<64, 6, kOffsets, true>())
                    : (nt ? kernel_ptr<64, 6, kOffsets, false, true>() : kernel_ptr<64, 6, kOffsets, false>());
     if (dyn_policy(width, kOffsets, nt, light)) a.queue = queue_slot(c, stream);
-    return launch(k, a, grid_for(c, count, k), stream);
+    rc = launch(k, a, grid_for(c, count, k), stream);
+    if (rc == MCHECKSUM_GPU_OK && gpu_msb(midx)) rc = swap_outputs(out, count, width, stream);
+    return rc;
 }
 
 // Large aligned CRC-64 payloads go to the work queue as kSplitBytes pieces
@@ -389,7 +428,9 @@ int launch_fixed(DevCtx *c, int idx, const void *pack, int width, int lg, const 
                                        Shape<64, kFixedAligned>::blocks_per_cu}
                              : KLaunch{crc64_batch_kernel<6, kFixedAligned, false, false, true>, Shape<64, kFixedAligned>::block,
                                        Shape<64, kFixedAligned>::blocks_per_cu};
-        return launch(k, a, grid_for(c, (uint64_t)count << sl, k), stream);
+        int rc = launch(k, a, grid_for(c, (uint64_t)count << sl, k), stream);
+        if (rc == MCHECKSUM_GPU_OK && gpu_msb(idx)) rc = swap_outputs(dev_out, count, width, stream);
+        return rc;
     }
     const KLaunch k = width == 32 ? pick_fixed<32>(lg, aligned, nt, light) : pick_fixed<64>(lg, aligned, nt, false);
     const uint64_t ppw = 64u >> lg;
@@ -402,7 +443,9 @@ int launch_fixed(DevCtx *c, int idx, const void *pack, int width, int lg, const 
     if (width == 64 && !dyn_policy(width, aligned ? kFixedAligned : kFixedGeneric, nt, false) &&
         units < (uint64_t)c->cus * (uint64_t)(k.block / 64))
         blocks = (unsigned)(units < (uint64_t)c->cus ? (units ? units : 1) : c->cus);
-    return launch(k, a, blocks, stream);
+    int rc = launch(k, a, blocks, stream);
+    if (rc == MCHECKSUM_GPU_OK && gpu_msb(idx)) rc = swap_outputs(dev_out, count, width, stream);
+    return rc;
 }
 
 }  // namespace mck

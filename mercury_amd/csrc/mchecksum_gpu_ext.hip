@@ -669,11 +669,7 @@ int get_ext(DevCtx *c, int idx, const void **out) {
             rc = 0;
         }
     } else {
-        crc_rmodel_t rm;
-        rm.width = m.width;
-        rm.rpoly = mck_reflect(m.poly, m.width);
-        rm.rinit = mck_reflect(m.init, m.width);
-        rm.xorout = m.xorout;
+        const crc_rmodel_t rm = gpu_rmodel(idx);
         bytes = m.width == 32 ? sizeof(crc32_shift_pack_t) : sizeof(crc64_shift_pack_t);
         host = calloc(1, bytes);
         if (host)
@@ -798,6 +794,8 @@ int mchecksum_gpu_checksum_segments(const char *hash_method, const uint64_t *dev
     }
     e = hipGetLastError();
     if (e != hipSuccess) return hip_err(e, "segment kernel launch");
+    // MSB-first model: the kernels' values are the CRCs byte-swapped (crc_gpu_layout.h)
+    if (gpu_msb(mck_model_index(hash_method))) return swap_outputs(dev_out, nobj, width, stream);
     return MCHECKSUM_GPU_OK;
 }
 
@@ -863,7 +861,8 @@ int mchecksum_gpu_checksum_xdr(const char *hash_method, const mchecksum_xdr_fiel
     int width = 0;
     const int idx = gpu_model(hash_method, &width);
     if (idx == -1) return set_err(MCHECKSUM_GPU_EMETHOD, "unknown hash method \"%s\"", hash_method ? hash_method : "(null)");
-    if (idx < 0) return set_err(MCHECKSUM_GPU_EMETHOD, "method \"%s\" has no GPU kernel (reflected 32/64-bit only)", hash_method);
+    if (idx < 0 || gpu_msb(idx))
+        return set_err(MCHECKSUM_GPU_EMETHOD, "method \"%s\" has no XDR kernel (reflected 32/64-bit only)", hash_method);
     if (!mchecksum_gpu_available()) return set_err(MCHECKSUM_GPU_ENODEV, "no HIP device");
     DevCtx *c = nullptr;
     const void *shift = nullptr;

@@ -82,7 +82,7 @@ static pthread_once_t g_shift_once = PTHREAD_ONCE_INIT;
 static void
 build_shift(void)
 {
-    const crc_rmodel_t m = {32, 0x82F63B78ULL, 0xFFFFFFFFULL, 0xFFFFFFFFULL};
+    const crc_rmodel_t m = {32, 0x82F63B78ULL, 0xFFFFFFFFULL, 0xFFFFFFFFULL, 0};
     uint64_t op[64];
     int s, p, b;
 

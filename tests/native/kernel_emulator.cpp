@@ -172,6 +172,26 @@ int main() {
                 if (e64 != g64) { fails++; if (fails < 10) printf("crc64 lg=%d len=%ld start=%ld %016lx vs %016lx\n", lg, (long)len, (long)start, (unsigned long)g64, (unsigned long)e64); }
             }
     }
+    // MSB-first model (CRC-64/ECMA-182, refin = refout = false): the kernels run
+    // the reflected model of the same polynomial conjugated by the per-byte bit
+    // reversal R (crc_gpu_layout.h); the output is the CRC byte-swapped
+    const oracle_model_t *me = oracle_model_by_name("crc64-ecma182");
+    auto refl = [](uint64_t v, int w) { uint64_t r = 0; for (int i = 0; i < w; i++) if ((v >> i) & 1) r |= 1ULL << (w - 1 - i); return r; };
+    crc_rmodel_t rme = {64, refl(0x42F0E1EBA9EA3693ULL, 64), crc_rev_bytes(64, refl(0, 64)), crc_rev_bytes(64, refl(0, 64)), 1};
+    for (int lg : {0, 3, 6}) {
+        static crc64_gpu_pack_t pe;
+        if (crc64_gpu_pack_build(&rme, lg, &pe)) {
+            printf("msb pack build failed\n");
+            return 1;
+        }
+        for (int64_t len : {0, 1, 7, 8, 9, 63, 64, 65, 1023, 1024, 4097, 65536})
+            for (int64_t start : {0, 1, 5, 8, 13, 16}) {
+                uint64_t e = oracle_crc_table(me, buf.data() + start, len);
+                uint64_t g = __builtin_bswap64(emu_crc64(&pe, buf.data(), (int64_t)buf.size(), start, len));
+                n++;
+                if (e != g) { fails++; if (fails < 10) printf("crc64-ecma182 lg=%d len=%ld start=%ld %016lx vs %016lx\n", lg, (long)len, (long)start, (unsigned long)g, (unsigned long)e); }
+            }
+    }
     printf("%d cases, %d failures\n", n, fails);
     return fails != 0;
 }

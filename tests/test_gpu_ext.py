@@ -53,14 +53,14 @@ def _want(oracle_mod, method, host, segs, first):
     return out
 
 
-@pytest.mark.parametrize("method", ["crc32c", "crc64"])
+@pytest.mark.parametrize("method", ["crc32c", "crc64", "crc64-ecma182"])
 @pytest.mark.parametrize("map_cap", [None, "0", "40"])
 def test_segments_random_objects(gpu, buf, oracle_mod, method, map_cap, monkeypatch):
     """map_cap: the CRC-64 queue pass finds each chunk's segment in the scan's
     chunk map; "0" forces the search over the chunk prefix sums, "40" a map
     too small for the list (searched too, after partial map writes)."""
     if map_cap is not None:
-        if method == "crc32c":
+        if method != "crc64":
             pytest.skip("the chunk map serves the CRC-64 queue pass only")
         monkeypatch.setenv("MCHECKSUM_GPU_SEG_MAP_CAP", map_cap)
     rng = np.random.default_rng(77 if method == "crc32c" else 78)

@@ -18,7 +18,10 @@ SEED_C2 = 0x4D43310000000002
 SEED_C3 = 0x4D43310000000003
 SEED_C4 = 0x4D43310000000004
 SEED_METRIC = 0x4D43310000000005
-METHODS = ["crc32c", "crc64"]
+# crc32 (IEEE, reflected) and crc64-ecma182 (MSB-first: run as the reflected
+# model conjugated by the per-byte bit reversal, outputs byte-swapped --
+# crc_gpu_layout.h) cover the other catalogue forms the GPU path takes
+METHODS = ["crc32c", "crc64", "crc32", "crc64-ecma182"]
 
 
 def _dev_bytes(torch, host: np.ndarray, pad: int = 64):
@@ -239,9 +242,10 @@ def test_gpu_matches_streaming_api(gpu, oracle_mod):
         assert c.get() == got
 
 
-@pytest.mark.parametrize("count,length,extra", [(37, 512 << 10, 0), (5, 2 << 20, 4096), (3, 16 << 20, 16),
-                                                (1, 1 << 20, 0), (9, 1 << 20, 0)])
-def test_crc64_split_pieces(gpu, oracle_mod, monkeypatch, count, length, extra):
+@pytest.mark.parametrize("count,length,extra,method", [(37, 512 << 10, 0, "crc64"), (5, 2 << 20, 4096, "crc64"),
+                                                       (3, 16 << 20, 16, "crc64"), (1, 1 << 20, 0, "crc64"),
+                                                       (9, 1 << 20, 0, "crc64"), (9, 1 << 20, 0, "crc64-ecma182")])
+def test_crc64_split_pieces(gpu, oracle_mod, monkeypatch, count, length, extra, method):
     """CRC-64 payloads of whole 256 KiB pieces go to the work queue piece by
     piece and are recombined with Z^n shifts (crc64_batch_kernel<..., SPLIT>):
     forced on with MCHECKSUM_GPU_SPLIT=1 at these small sizes, equal to the
@@ -250,11 +254,26 @@ def test_crc64_split_pieces(gpu, oracle_mod, monkeypatch, count, length, extra):
     stride = length + extra
     host = oracle_mod.splitmix_bytes(stride * (count - 1) + length, 0x5B17 + count)
     dev = _dev_bytes(torch, host)
-    want = oracle_mod.batch_fixed("crc64", host, stride, length, count, nthreads=8)
+    want = oracle_mod.batch_fixed(method, host, stride, length, count, nthreads=8)
     stale = torch.full((count,), -1, dtype=torch.int64, device="cuda")  # the split path zeroes out[] itself
     monkeypatch.setenv("MCHECKSUM_GPU_SPLIT", "1")
-    got = gpu.as_unsigned(gpu.checksum_fixed("crc64", dev, length, count=count, stride=stride, out=stale))
+    got = gpu.as_unsigned(gpu.checksum_fixed(method, dev, length, count=count, stride=stride, out=stale))
     monkeypatch.setenv("MCHECKSUM_GPU_SPLIT", "0")
-    plain = gpu.as_unsigned(gpu.checksum_fixed("crc64", dev, length, count=count, stride=stride))
+    plain = gpu.as_unsigned(gpu.checksum_fixed(method, dev, length, count=count, stride=stride))
     assert np.array_equal(got.astype(np.uint64), want)
     assert np.array_equal(plain.astype(np.uint64), want)
+
+
+def test_msb_first_method_refuses_verify(gpu, oracle_mod):
+    """MSB-first methods checksum on the GPU (outputs byte-swapped after the
+    launch); in-kernel verify would compare swapped values, so it refuses."""
+    import torch
+    host = oracle_mod.splitmix_bytes(4096, 3)
+    t = _dev_bytes(torch, host)
+    off = np.array([0, 1000, 4096], dtype=np.uint64)
+    offs = torch.from_numpy(off.astype(np.int64)).cuda()
+    exp = torch.zeros(2, dtype=torch.int64, device="cuda")
+    with pytest.raises(gpu.GpuChecksumError):
+        gpu.verify_offsets("crc64-ecma182", t, offs, exp)
+    got = gpu.as_unsigned(gpu.checksum_offsets("crc64-ecma182", t, offs))
+    assert got.tolist() == [oracle_mod.crc("crc64-ecma182", host[:1000]), oracle_mod.crc("crc64-ecma182", host[1000:])]
