@@ -56,7 +56,7 @@
 #define MCHECKSUM_GPU_EINVAL    (-1) /* bad argument */
 #define MCHECKSUM_GPU_ENODEV    (-2) /* no usable HIP device */
 #define MCHECKSUM_GPU_EMETHOD   (-3) /* method not supported on GPU (16-bit methods on the
-                                         payload paths; MSB-first ones on verify and XDR) */
+                                         payload paths; MSB-first ones on XDR) */
 #define MCHECKSUM_GPU_EHIP      (-4) /* HIP runtime error (see error string) */
 
 #ifdef __cplusplus

@@ -167,6 +167,9 @@ struct BatchArgs {
     // 2^split_log2 pieces of kSplitBytes, recombined with the Z^n shift pack
     const void *shift;
     uint32_t split_log2;
+    // MSB-first model on a verify call: the kernel's value is the CRC
+    // byte-swapped (crc_gpu_layout.h), so swap before comparing
+    uint32_t bswap;
 };
 // Piece size of a split payload: 256 KiB = 256 steps of the G = 64 loop.
 constexpr uint64_t kSplitBytes = 256u << 10;
@@ -1038,6 +1041,10 @@ __device__ unsigned long long g_mck_trace[3 * kTraceWaves];
 template <typename T, bool VERIFY>
 __device__ __forceinline__ void emit(const BatchArgs &a, uint64_t p, T v) {
     if (VERIFY) {
+        if (a.bswap) {
+            if constexpr (sizeof(T) == 8) v = (T)__builtin_bswap64((uint64_t)v);
+            else v = (T)__builtin_bswap32((uint32_t)v);
+        }
         const bool bad = reinterpret_cast<const T *>(a.expected)[p] != v;
         if (a.status) a.status[p] = bad ? 1 : 0;
         if (bad && a.mismatches) atomicAdd(a.mismatches, 1u);

@@ -347,8 +347,7 @@ int do_offsets(const char *method, const void *base, const uint64_t *offsets, si
     if (msg && width != 32)
         return set_err(MCHECKSUM_GPU_EMETHOD, "message verify carries a 32-bit header hash: crc32c only");
     const int midx = gpu_model(method, &width);
-    if (verify && gpu_msb(midx))
-        return set_err(MCHECKSUM_GPU_EMETHOD, "verify of MSB-first method \"%s\": checksum and compare instead", method);
+    a.bswap = verify && gpu_msb(midx) ? 1u : 0u;  // checksum calls swap after the launch
     KLaunch k;
     // The offsets table stays on the device, so size the batch by its count:
     // 8192+ payloads of the C4 mix are ~270 MB and up.
@@ -366,7 +365,7 @@ int do_offsets(const char *method, const void *base, const uint64_t *offsets, si
                    : (nt ? kernel_ptr<64, 6, kOffsets, false, true>() : kernel_ptr<64, 6, kOffsets, false>());
     if (dyn_policy(width, kOffsets, nt, light)) a.queue = queue_slot(c, stream);
     rc = launch(k, a, grid_for(c, count, k), stream);
-    if (rc == MCHECKSUM_GPU_OK && gpu_msb(midx)) rc = swap_outputs(out, count, width, stream);
+    if (rc == MCHECKSUM_GPU_OK && gpu_msb(midx) && !verify) rc = swap_outputs(out, count, width, stream);
     return rc;
 }
 

@@ -264,16 +264,24 @@ def test_crc64_split_pieces(gpu, oracle_mod, monkeypatch, count, length, extra, 
     assert np.array_equal(plain.astype(np.uint64), want)
 
 
-def test_msb_first_method_refuses_verify(gpu, oracle_mod):
-    """MSB-first methods checksum on the GPU (outputs byte-swapped after the
-    launch); in-kernel verify would compare swapped values, so it refuses."""
+def test_msb_first_method_verify(gpu, oracle_mod):
+    """MSB-first methods: checksum outputs are byte-swapped after the launch,
+    verify swaps the kernel's value before comparing (BatchArgs::bswap) --
+    both agree with the oracle, and a flipped bit is flagged where it is."""
     import torch
-    host = oracle_mod.splitmix_bytes(4096, 3)
+    rng = np.random.default_rng(11)
+    off = np.zeros(401, dtype=np.uint64)
+    off[1:] = np.cumsum(rng.integers(0, 9000, 400))
+    host = oracle_mod.splitmix_bytes(int(off[-1]) + 16, 3)[:int(off[-1])]
     t = _dev_bytes(torch, host)
-    off = np.array([0, 1000, 4096], dtype=np.uint64)
     offs = torch.from_numpy(off.astype(np.int64)).cuda()
-    exp = torch.zeros(2, dtype=torch.int64, device="cuda")
-    with pytest.raises(gpu.GpuChecksumError):
-        gpu.verify_offsets("crc64-ecma182", t, offs, exp)
+    want = oracle_mod.batch_offsets("crc64-ecma182", host, off, nthreads=8)
     got = gpu.as_unsigned(gpu.checksum_offsets("crc64-ecma182", t, offs))
-    assert got.tolist() == [oracle_mod.crc("crc64-ecma182", host[:1000]), oracle_mod.crc("crc64-ecma182", host[1000:])]
+    assert np.array_equal(got.astype(np.uint64), want)
+    exp = torch.from_numpy(want.astype(np.uint64).view(np.int64)).cuda()
+    st, bad = gpu.verify_offsets("crc64-ecma182", t, offs, exp)
+    assert int(bad.item()) == 0 and int(st.sum().item()) == 0
+    victim = int(np.nonzero(np.diff(off) > 0)[0][7])
+    t[int(off[victim])] ^= 0x20
+    st, bad = gpu.verify_offsets("crc64-ecma182", t, offs, exp)
+    assert int(bad.item()) == 1 and np.nonzero(st.cpu().numpy())[0].tolist() == [victim]
