@@ -9,7 +9,8 @@
  *
  *   value[i] == mchecksum_get() after mchecksum_update(payload_i, len_i)
  *
- * bit for bit, for every method the GPU supports (crc32c, crc64).  The
+ * bit for bit, for every method the GPU supports (every 32/64-bit catalogue
+ * method: crc32c, crc32, crc64 and its variants, MSB-first ECMA-182 included).  The
  * whole-buffer form is exact because, in Mercury's default non-XDR build, the
  * proc checksum is the CRC of the contiguous serialized bytes
  * buf[0 : hg_proc_get_size_used) (src/mercury_proc.h:124-143,162-181;
@@ -130,7 +131,7 @@ mchecksum_gpu_verify_messages(const char *hash_method, const void *dev_buf,
  * outside [first[0], first[nobj]) are ignored.  dev_work: caller-owned device
  * scratch (8-byte aligned) of at least mchecksum_gpu_segments_work_size(nseg)
  * bytes, not shared with a concurrent call (SIZE_MAX for nseg > 2^40, which
- * is rejected).  crc32c and crc64.  Segments are
+ * is rejected).  Every 32/64-bit method.  Segments are
  * cut into 256 KiB chunks hashed in parallel and recombined with GF(2) shift
  * operators, so one huge segment still spreads over the whole GPU. */
 MCHECKSUM_PUBLIC size_t
