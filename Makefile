@@ -47,7 +47,10 @@ $(LIB): $(COBJS) $(GOBJS) | $(LIBDIR)
 $(BUILD)/qfault_gpu.o: $(CSRC)/mchecksum_gpu.hip $(wildcard $(CSRC)/*.h) include/mchecksum_gpu.h | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -DMCK_QFAULT_TEST=1 $(INC) -c $< -o $@
 
-$(QFAULTLIB): $(COBJS) $(BUILD)/qfault_gpu.o $(BUILD)/mchecksum_gpu_ext.o
+$(BUILD)/qfault_gpu_ext.o: $(CSRC)/mchecksum_gpu_ext.hip $(wildcard $(CSRC)/*.h) include/mchecksum_gpu.h | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -DMCK_QFAULT_TEST=1 $(INC) -c $< -o $@
+
+$(QFAULTLIB): $(COBJS) $(BUILD)/qfault_gpu.o $(BUILD)/qfault_gpu_ext.o
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^ -lpthread
 
 $(BENCHLIB): $(BUILD)/bench_datagen.o | $(LIBDIR)

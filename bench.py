@@ -5,15 +5,17 @@ Metric (BASELINE.json): GiB/s checksummed (device-resident), CRC32c,
 64K x 64 KiB payloads.  One "step" = one batch launch over the whole
 per-GPU batch (65536 payloads of 64 KiB = 4 GiB), inputs already in HBM.
 
-Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
-each rank owns a contiguous shard of a global batch (weak scaling: per-GPU
-work fixed), generated on its own device; no collective in the timed region.
-After timing, RCCL all_gather of the per-shard CRC arrays to check the
-gathered result and an all_reduce(MAX) of the timings.
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N,
+or bench.py --gpus N, which starts those ranks itself): each rank owns a
+contiguous share of ONE global batch, generated on its own device; no
+collective in the timed region.  After timing: RCCL all_gather of the
+per-share CRC arrays (global payload order) and of the timings.
 
 Prints ONE JSON line on rank 0 (contract in the task statement), with
-`roofline` (HIP-event kernel time vs HBM peak) and `cpu_baseline` (oracle on
-this host's cores, N=1 only).
+`roofline` (HIP-event kernel time vs HBM peak; `traffic` from the committed
+PMC profile, scaled to rank 0's share at N > 1) and `cpu_baseline` (the
+oracle timed on this host's cores, at every N, on rank 0 after timing) --
+the oracle also checks the gathered CRCs of every share (`parity`).
 """
 from __future__ import annotations
 
@@ -28,8 +30,8 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-HBM_PEAK_GBS = 8000.0
-SEGS_PER_OBJECT = 4  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md:36
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md:36
+SEGS_PER_OBJECT = 4
 
 CONFIGS = {
     # name: (method, count, length, seed, layout)
@@ -49,10 +51,17 @@ CONFIGS = {
     "msgs": ("crc32c", 262144, None, 0x4D43310000000004, "messages"),
     # BASELINE configs[0]: host CPU, through the drop-in streaming API
     "c1": ("crc32c", 1024, 4096, 0x4D43310000000001, "cpu"),
+    # 8(f) 4: C4's payloads as hg_perf_proc_iovec messages serialized in XDR
+    # mode (Testing/perf/hg/mercury_perf.c:897-923; src/mercury_proc.h:110-160):
+    # a big-endian u32 length, the bytes, zero pad to 4 -- while the checksum
+    # covers the host-order length and the bytes (mchecksum_gpu_checksum_xdr)
+    "xdr": ("crc32c", 262144, None, 0x4D43310000000004, "xdr"),
 }
 # configs whose count is the GLOBAL batch, split over the ranks (strong
 # scaling); the others give every rank a batch of that size (weak scaling)
-STRONG = {"c5", "c4", "msgs"}
+STRONG = {"c5", "c4", "msgs", "xdr"}
+# hg_perf_proc_iovec's XDR schema: INT(4) length, OPAQUE_LEN bytes
+XDR_IOVEC = [(0, 4), (2, 0)]
 
 
 def parse():
@@ -154,6 +163,8 @@ def main():
         plan = batch_shard(rank, world, global_count, length)
     elif layout in ("offsets", "messages"):
         plan = batch_shard(rank, world, global_count, offsets_global=varlen_offsets(seed, global_count))
+    elif layout == "xdr":
+        plan = batch_shard(rank, world, global_count, offsets_global=xdr_offsets(seed, global_count))
     if plan is not None:
         count = plan.count
     stream = torch.cuda.current_stream()
@@ -200,6 +211,26 @@ def main():
         mism = torch.zeros(1, dtype=torch.int32, device=dev)
         G.verify_messages(data, msg_dev, status=status, mismatches=mism, offsets_host=msg_host)  # validates once
         run = lambda out: G.verify_messages(data, msg_dev, status=status, mismatches=mism)  # noqa: E731
+    elif layout == "xdr":
+        # the rank's messages: splitmix bytes, then each message's big-endian
+        # length word and zero pad written over them
+        from mercury_amd.workload import varlen_lengths
+        offsets_host = plan.offsets
+        payload_bytes = int(offsets_host[-1] - offsets_host[0])  # message bytes (read)
+        data = torch.empty(plan.nbytes + 64, dtype=torch.uint8, device=dev)
+        G.fill_splitmix(data, seed, first_word=plan.first_word)
+        lens = varlen_lengths(seed, global_count)[plan.first:plan.first + count].astype(np.int64)
+        msg_dev = torch.from_numpy(offsets_host.astype(np.int64)).to(dev)
+        lens_dev = torch.from_numpy(lens).to(dev)
+        for k in range(4):
+            data[msg_dev[:-1] + k] = ((lens_dev >> (24 - 8 * k)) & 0xFF).to(torch.uint8)
+        for k in range(1, 4):  # pad bytes: 4 + len .. 4 + RNDUP(len)
+            sel = (-lens_dev) % 4 >= k
+            data[(msg_dev[:-1] + 4 + lens_dev + k - 1)[sel]] = 0
+        offsets_dev = msg_dev
+        xout = torch.empty(count, dtype=G.out_dtype(method), device=dev)
+        G.checksum_xdr(method, data, msg_dev, XDR_IOVEC, offsets_host=offsets_host, out=xout)  # validates once
+        run = lambda out: G.checksum_xdr(method, data, msg_dev, XDR_IOVEC, out=out)  # noqa: E731
     else:
         offsets_host = plan.offsets
         payload_bytes = int(offsets_host[-1] - offsets_host[0])
@@ -276,15 +307,15 @@ def main():
         verify_note = (f"{args.steps + args.warmup + 1} verify launches: {bad_before} mismatches; one flipped bit "
                        f"flagged {flagged} (expected [{victim}])")
         crcs = sender  # the sender-side CRCs, checked against the oracle below
-    if world > 1 and layout != "messages":
+    if world > 1:
         # RCCL all_gather of the per-rank CRC arrays (padded to the largest
-        # shard: ranks may hold different counts), then trimmed in rank order
+        # shard: ranks may hold different counts), then trimmed in rank order:
+        # the global batch's CRCs in global payload order (messages: the
+        # sender's interleaved header/payload pieces, two per message)
         counts = plan.counts if plan is not None else [count] * world
-        mine = torch.zeros(max(counts), dtype=crcs.dtype, device=coll_dev)
-        mine[:count] = crcs[:count].to(coll_dev)
-        gathered = [torch.empty_like(mine) for _ in range(world)]
-        dist.all_gather(gathered, mine)
-        crcs = torch.cat([g[:c] for g, c in zip(gathered, counts)])
+        if layout == "messages":
+            counts = [2 * c for c in counts]
+        crcs = gather_shares(dist, crcs, counts, world, coll_dev)
     got = G.as_unsigned(crcs) if rank == 0 else None
 
     bytes_all = torch.tensor([float(payload_bytes)], dtype=torch.float64, device=coll_dev)
@@ -293,7 +324,7 @@ def main():
     total_bytes = float(bytes_all[0]) * args.steps  # every rank checksummed its shard once per step
     gib_s = total_bytes / wall_max / 2**30
     out_bytes = count * (4 if G.out_dtype(method) == torch.int32 else 8)
-    alg_bytes = payload_bytes + out_bytes + (8 * (count + 1) if layout == "offsets" else 0) + \
+    alg_bytes = payload_bytes + out_bytes + (8 * (count + 1) if layout in ("offsets", "xdr") else 0) + \
         (16 * count * SEGS_PER_OBJECT + 8 * (count + 1) if layout == "segments" else 0)
     if layout == "messages":  # messages read (headers included), 1 status byte each, the offsets table
         alg_bytes = payload_bytes + count + 8 * (count + 1)
@@ -301,70 +332,71 @@ def main():
 
     result = None
     if rank == 0:
-        # HBM bytes per launch cannot be counted inside this process: they come
-        # from the committed rocprofv3 PMC passes of this same command
-        # (tools/gpu_pmc_traffic.sh -> profiles/pmc_traffic_<config>.json)
-        traffic, traffic_src = None, None
-        pmc = os.path.join(ROOT, "profiles", f"pmc_traffic_{args.config}.json")
-        if os.path.exists(pmc) and world == 1:
-            try:
-                traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
-                traffic_src = (f"profiles/pmc_traffic_{args.config}.json (rocprofv3 FETCH_SIZE + WRITE_SIZE passes "
-                               "of this config, committed; not measured in this run)")
-            except Exception:
-                traffic = None
-        metric = {"metric": "GiB/s checksummed (device-resident), CRC32c, 64K x 64 KiB payloads",
-                  "c5": "GiB/s checksummed (device-resident), CRC32c, 1M x 64 KiB payloads split over the GPUs (C5)"}
-        result = {
-            "metric": metric.get(args.config, f"GiB/s checksummed (device-resident), {args.config}"),
-            "value": round(gib_s, 2),
-            "unit": "GiB/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(wall_max / args.steps * 1e3, 4),
-            "higher_is_better": True,
-            "scaling": "strong" if strong else "weak",
-            "vs_baseline": None,
-            "dtype": "u8",
-            "data": "synthetic (splitmix64 bytes generated on device)",
-            "config": {"workload": f"{args.config}: {method} over {global_count} x "
-                       f"{length if length else 'U[64B,64KiB]'} B payloads"
-                       + (" (offsets table)" if layout == "offsets" else "")
-                       + (" as Mercury messages, verified in place" if layout == "messages" else "")
-                       + (f" ({SEGS_PER_OBJECT} scattered segments each)" if layout == "segments" else "")
-                       + (f", one global batch split over {world} GPUs" if world > 1 and layout != "segments"
-                          else f", per GPU" if world > 1 else ""),
-                       "method": method, "global_batch": global_count, "payloads_rank0": count,
-                       "payload_bytes": length, "bytes_rank0": payload_bytes,
-                       "lanes_per_payload": G.lanes_per_payload(method, length or 65536) if layout == "fixed" else 64,
-                       "parallelism": f"shard{world}"},
-            "world_size": dist.get_world_size() if world > 1 else 1,
-            "per_rank": [{"rank": r, "wall_ms_per_step": round(w / args.steps * 1e3, 4), "kernel_ms": round(k, 4)}
-                         for r, (w, k) in enumerate(per_rank)],
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel_ms": round(kern_ms_max, 4), "algorithmic_bytes_per_launch": alg_bytes},
-        }
-        if world == 1 and not args.no_cpu_baseline:
-            # the only leg that runs the oracle: timed on a bounded sample, and
-            # the checker of the GPU's values (that sample + random payloads)
-            result["cpu_baseline"], result["parity"] = cpu_baseline(
-                method, seed, length, offsets_host, got, args.cpu_seconds, args.parity_samples,
-                segments=layout == "segments")
-        elif world > 1 and layout == "messages":
-            result["parity"] = "per-rank verify counters (see verify)"
-        elif world > 1:
-            result["parity"] = cross_rank_check(G, method, seed, length, got, world, dev, args.parity_samples,
-                                                layout, global_count, count)
-        else:
-            result["parity"] = "unchecked (--no-cpu-baseline)"
-        if verify_note:
-            result["verify"] = verify_note
+        from types import SimpleNamespace
+        result = report(args, SimpleNamespace(
+            config=args.config, method=method, seed=seed, length=length, layout=layout, strong=strong,
+            global_count=global_count, count=count, plan=plan, payload_bytes=payload_bytes, alg_bytes=alg_bytes,
+            gib_s=gib_s, wall_max=wall_max, kern_ms_max=kern_ms_max, achieved=achieved, per_rank=per_rank,
+            world=world, got=got, offsets_host=offsets_host, verify_note=verify_note,
+            lanes=G.lanes_per_payload(method, length or 65536) if layout == "fixed" else 64))
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    return result
+
+
+def report(args, r):
+    """Rank 0's JSON line of one run (r: the run's shape, shares, timings and
+    gathered CRCs, assembled by main).  The oracle runs here, after timing, at
+    every N: the CPU baseline, and the parity check of every rank's share."""
+    traffic, traffic_src = pmc_traffic(r.config, r.world, r.alg_bytes)
+    metric = {"metric": "GiB/s checksummed (device-resident), CRC32c, 64K x 64 KiB payloads",
+              "c5": "GiB/s checksummed (device-resident), CRC32c, 1M x 64 KiB payloads split over the GPUs (C5)"}
+    workload = (f"{r.config}: {r.method} over {r.global_count} x {r.length if r.length else 'U[64B,64KiB]'} B payloads"
+                + (" (offsets table)" if r.layout == "offsets" else "")
+                + (" as Mercury messages, verified in place" if r.layout == "messages" else "")
+                + (" as hg_perf_proc_iovec messages in XDR mode" if r.layout == "xdr" else "")
+                + (f" ({SEGS_PER_OBJECT} scattered segments each)" if r.layout == "segments" else "")
+                + (f", one global batch split over {r.world} GPUs" if r.world > 1 and r.layout != "segments"
+                   else ", per GPU" if r.world > 1 else ""))
+    result = {
+        "metric": metric.get(r.config, f"GiB/s checksummed (device-resident), {r.config}"),
+        "value": round(r.gib_s, 2),
+        "unit": "GiB/s",
+        "n_gpus": r.world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(r.wall_max / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "strong" if r.strong else "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (splitmix64 bytes generated on device)",
+        "config": {"workload": workload, "method": r.method, "global_batch": r.global_count,
+                   "payloads_rank0": r.count, "payload_bytes": r.length, "bytes_rank0": r.payload_bytes,
+                   "lanes_per_payload": r.lanes, "parallelism": f"shard{r.world}"},
+        "world_size": r.world,
+        "per_rank": [{"rank": i, "wall_ms_per_step": round(w / args.steps * 1e3, 4), "kernel_ms": round(k, 4)}
+                     for i, (w, k) in enumerate(r.per_rank)],
+        "roofline": {"bound": "hbm", "achieved": round(r.achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(r.achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
+                     "kernel_ms": round(r.kern_ms_max, 4), "algorithmic_bytes_per_launch": r.alg_bytes},
+    }
+    if not args.no_cpu_baseline:
+        # the only leg that runs the oracle: timed on a bounded sample on this
+        # host's cores, and the checker of the gathered CRCs -- that sample,
+        # the first and last payload of every rank's share and random payloads
+        # of the whole global batch
+        result["cpu_baseline"], result["parity"] = cpu_baseline(
+            r.method, r.seed, r.length, global_offsets(r.layout, r.seed, r.global_count, r.offsets_host), r.got,
+            args.cpu_seconds, args.parity_samples, segments=r.layout == "segments",
+            world=r.world, count0=r.count, share_firsts=share_firsts(r.plan, r.layout, r.world, r.count),
+            xdr=r.layout == "xdr")
+    else:
+        result["parity"] = "unchecked (--no-cpu-baseline)"
+    if r.verify_note:
+        result["verify"] = r.verify_note
     return result
 
 
@@ -439,12 +471,21 @@ def _cpu_model():
     return "unknown"
 
 
-def cpu_baseline(method, seed, length, offsets_host, got, budget_s, samples, segments=False):
-    """The CPU leg (N=1, rank 0): the oracle (CPU restatement of mchecksum --
-    the reference's own mchecksum is absent, so kind = "port") timed on this
-    host's cores over a bounded sample of the same workload (the first n
-    payloads), whose CRCs then check the GPU's values for those payloads; plus
-    `samples` random payloads from the whole batch."""
+def cpu_baseline(method, seed, length, offsets_host, got, budget_s, samples, segments=False, world=1, count0=None,
+                 share_firsts=(), xdr=False):
+    """The CPU leg (rank 0, after timing, at every N): the oracle (CPU
+    restatement of mchecksum -- the reference's own mchecksum is absent, so
+    kind = "port") timed on this host's cores over a bounded sample of the
+    same workload (the first n payloads of the global batch), whose CRCs then
+    check the gathered GPU values for those payloads; plus the first and last
+    payload of every rank's share (share_firsts) and `samples` random payloads
+    of the whole global batch.  `got`: the gathered CRCs in global order;
+    offsets_host: the global offsets table (None for fixed layouts); segments:
+    rank r's count0 objects come from seed ^ r (weak scaling); xdr: the
+    messages of the xdr config, whose checksum covers the host-order length
+    and the payload bytes (the oracle is timed over those hashed streams --
+    the CRC work of an XDR build's mchecksum_update calls, not its XDR
+    decoding -- and the rate is quoted in message bytes, like the GPU's)."""
     from oracle import oracle as O
     # `nproc` threads (BASELINE.md "Thread counts"): every CPU this process may
     # run on -- capped by the cgroup CPU quota when the box sets one (the GPU
@@ -455,22 +496,49 @@ def cpu_baseline(method, seed, length, offsets_host, got, budget_s, samples, seg
     threads = max(1, min(256, affinity, int(quota[0]) if quota else affinity))
     variant = "sse42" if method == "crc32c" else "slice8"
     slots = None
+    count0 = len(got) if count0 is None else count0
     if segments:
         from mercury_amd.workload import segment_slots
-        slots = segment_slots(seed, len(got) * SEGS_PER_OBJECT)
-        n = 256
+        slots = segment_slots(seed, count0 * SEGS_PER_OBJECT)
+        rank_slots = {0: slots}
+        n = min(256, count0)
         host = np.concatenate([_segment_object_bytes(O, seed, length, j, slots) for j in range(n)])
         runv = lambda k, v, th: O.batch_fixed(method, host, length, length, k, variant=v, nthreads=th)  # noqa: E731
         sample_bytes = n * length
         what = f"the first {n} objects ({SEGS_PER_OBJECT} x {length // SEGS_PER_OBJECT} B segments, gathered)"
+    elif xdr:
+        import struct
+        from mercury_amd.workload import varlen_lengths
+        xlens = varlen_lengths(seed, len(offsets_host) - 1).astype(np.int64)
+        n = min(int(np.searchsorted(offsets_host, np.uint64(256 << 20))), len(offsets_host) - 1)
+        raw = O.splitmix_bytes(int(offsets_host[n]), seed)
+        parts = []
+        for i in range(n):
+            o = int(offsets_host[i]) + 4
+            parts += [np.frombuffer(struct.pack("<I", int(xlens[i])), dtype=np.uint8), raw[o:o + int(xlens[i])]]
+        host = np.concatenate(parts)
+        hoff = np.zeros(n + 1, dtype=np.uint64)
+        np.cumsum(np.uint64(4) + xlens[:n].astype(np.uint64), out=hoff[1:])
+        runv = lambda k, v, th: O.batch_offsets(method, host, hoff[:k + 1], variant=v, nthreads=th)  # noqa: E731
+        sample_bytes = int(offsets_host[n])
+        what = (f"the first {n} messages ({sample_bytes} B): the hashed streams (host-order length + payload "
+                f"bytes) an XDR build feeds mchecksum_update")
+
+        def xdr_message(gi):  # the message's bytes as the device holds them, and its hashed stream
+            lo, hi, ln = int(offsets_host[gi]), int(offsets_host[gi + 1]), int(xlens[gi])
+            w0 = lo // 8
+            b = O.splitmix_bytes(hi - w0 * 8, seed, first_word=w0)[lo - w0 * 8:]
+            payload = b[4:4 + ln].tobytes()
+            msg = struct.pack(">I", ln) + payload + bytes(hi - lo - 4 - ln)
+            return msg, struct.pack("<I", ln) + payload
     elif offsets_host is None:
-        n = 4096 if length <= 65536 else 256
+        n = min(4096 if length <= 65536 else 256, len(got))
         host = O.splitmix_bytes(n * length, seed)
         runv = lambda k, v, th: O.batch_fixed(method, host, length, length, k, variant=v, nthreads=th)  # noqa: E731
         sample_bytes = n * length
         what = f"{n} x {length} B"
     else:
-        n = int(np.searchsorted(offsets_host, np.uint64(256 << 20)))  # ~256 MiB of whole payloads
+        n = min(int(np.searchsorted(offsets_host, np.uint64(256 << 20))), len(offsets_host) - 1)  # ~256 MiB
         host = O.splitmix_bytes(int(offsets_host[n]), seed)
         sub = np.ascontiguousarray(offsets_host[:n + 1])
         runv = lambda k, v, th: O.batch_offsets(method, host, sub[:k + 1], variant=v, nthreads=th)  # noqa: E731
@@ -515,11 +583,18 @@ def cpu_baseline(method, seed, length, offsets_host, got, budget_s, samples, seg
     bad = int(np.count_nonzero(got[:n] != want))
     rng = np.random.default_rng(1234)
     total = len(got)
-    idx = np.unique(np.concatenate([[total - 1], rng.integers(n, total, samples)])) if total > n else []
+    idx = np.unique(np.concatenate([[total - 1], np.asarray(share_firsts, dtype=np.int64),
+                                    rng.integers(n, total, samples)]).astype(np.int64)) if total > n else []
+    idx = [int(i) for i in idx if int(i) >= n]
     for gi in idx:
         gi = int(gi)
-        if segments:
-            w = O.crc(method, _segment_object_bytes(O, seed, length, gi, slots))
+        if xdr:
+            w = O.crc(method, xdr_message(gi)[1])
+        elif segments:
+            r, j = divmod(gi, count0)
+            if r not in rank_slots:
+                rank_slots[r] = segment_slots(seed ^ r, count0 * SEGS_PER_OBJECT)
+            w = O.crc(method, _segment_object_bytes(O, seed ^ r, length, j, rank_slots[r]))
         elif offsets_host is None:
             w = O.splitmix_batch_fixed(method, seed, length, length, gi, 1)[0]
         else:
@@ -528,55 +603,95 @@ def cpu_baseline(method, seed, length, offsets_host, got, budget_s, samples, seg
             b = O.splitmix_bytes(hi - w0 * 8, seed, first_word=w0)
             w = O.crc(method, b[lo - w0 * 8:])
         bad += int(got[gi] != w)
+    if xdr:  # the oracle's XDR restatement (decode the wire bytes by the schema) on one message
+        msg, stream = xdr_message(0)
+        schema = [(O.XDR_INT, 4), (O.XDR_OPAQUE_LEN, 0)]
+        bad += int(O.xdr_hashed_stream(schema, msg) != stream or O.crc(method, stream) != got[0])
     checked = n + len(idx)
-    parity = f"bit-exact ({checked} payloads vs oracle)" if bad == 0 else f"MISMATCH {bad}/{checked}"
+    where = f" across all {world} shares" if world > 1 else ""
+    parity = f"bit-exact ({checked} payloads{where} vs oracle)" if bad == 0 else f"MISMATCH {bad}/{checked}{where}"
     return base, parity
 
 
-def cross_rank_check(G, method, seed, length, got, world, dev, samples, layout, global_count, count0):
-    """N>1 (rank 0): regenerate sampled payloads of EVERY rank's share on rank
-    0's GPU and recompute them through the same entry point; the gathered CRCs
-    (global payload order) must agree.  Kernel parity itself is the N=1 oracle
-    check and tests/."""
-    if got is None:
-        return None
+def xdr_offsets(seed, count):
+    """Message offsets of the xdr config: message i = 4-byte length + C4's
+    len_i payload bytes + zero pad to a multiple of 4 (xdr_opaque)."""
+    from mercury_amd.workload import varlen_lengths
+    lens = varlen_lengths(seed, count)
+    off = np.zeros(count + 1, dtype=np.uint64)
+    np.cumsum(np.uint64(4) + (lens + np.uint64(3)) // np.uint64(4) * np.uint64(4), out=off[1:])
+    return off
+
+
+def gather_shares(dist, crcs, counts, world, coll_dev):
+    """all_gather of the per-rank CRC arrays, padded to the largest share
+    (ranks may hold different counts), trimmed and concatenated in rank order
+    -- shares are contiguous ranges of the global batch, so the result is in
+    global payload order."""
     import torch
+    rank = dist.get_rank()
+    mine = torch.zeros(max(counts), dtype=crcs.dtype, device=coll_dev)
+    mine[:counts[rank]] = crcs[:counts[rank]].to(coll_dev)
+    gathered = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(gathered, mine)
+    return torch.cat([g[:c] for g, c in zip(gathered, counts)])
+
+
+def global_offsets(layout, seed, global_count, offsets_host):
+    """The host offsets table of the WHOLE global batch, for the oracle check
+    (None for fixed-size layouts): C4's packed layout regenerated from its seed;
+    for messages the sender's interleaved (header, payload) pieces."""
     from mercury_amd.workload import varlen_offsets
-    rng = np.random.default_rng(4321)
-    bad = checked = 0
-    if layout == "segments":  # weak: rank r's objects from seed ^ r, count0 per rank
-        from mercury_amd.workload import segment_slots
-        seg = length // SEGS_PER_OBJECT
-        for r in range(world):
-            slots = segment_slots(seed ^ r, count0 * SEGS_PER_OBJECT)
-            for i in np.unique(np.concatenate([[0, count0 - 1], rng.integers(0, count0, max(1, samples // world))])):
-                parts = []
-                for q in range(SEGS_PER_OBJECT):
-                    t = torch.empty(seg + 64, dtype=torch.uint8, device=dev)
-                    G.fill_splitmix(t, seed ^ r, first_word=int(slots[int(i) * SEGS_PER_OBJECT + q]) * seg // 8)
-                    parts.append(t[:seg])
-                bad += int(G.as_unsigned(G.checksum_segments(method, parts))[0] != got[r * count0 + int(i)])
-                checked += 1
+    if layout == "offsets":
+        return varlen_offsets(seed, global_count)
+    if layout == "xdr":
+        return xdr_offsets(seed, global_count)
+    if layout == "messages":
+        msg = varlen_offsets(seed, global_count)
+        inter = np.empty(2 * global_count + 1, dtype=np.uint64)
+        inter[0::2] = msg
+        inter[1::2] = msg[:-1] + np.uint64(20)
+        return inter
+    return None
+
+
+def share_firsts(plan, layout, world, count0):
+    """Indices (into the gathered CRC array) of the first and last payload of
+    every rank's share, so the oracle check touches every share."""
+    if layout == "segments":  # weak: count0 objects per rank
+        firsts, counts = [r * count0 for r in range(world)], [count0] * world
+    elif plan is not None:
+        firsts, counts = plan.firsts, plan.counts
     else:
-        off = varlen_offsets(seed, global_count) if layout == "offsets" else None
-        idx = np.unique(np.concatenate([[0, global_count - 1], rng.integers(0, global_count, samples)]))
-        for i in idx:
-            i = int(i)
-            if off is None:
-                buf = torch.empty(length + 64, dtype=torch.uint8, device=dev)
-                G.fill_splitmix(buf, seed, first_word=i * length // 8)
-                v = G.checksum_fixed(method, buf, length, count=1)
-            else:
-                lo, hi = int(off[i]), int(off[i + 1])
-                w0 = lo // 8
-                buf = torch.empty(hi - w0 * 8 + 64, dtype=torch.uint8, device=dev)
-                G.fill_splitmix(buf, seed, first_word=w0)
-                t = torch.tensor([lo - w0 * 8, hi - w0 * 8], dtype=torch.int64, device=dev)
-                v = G.checksum_offsets(method, buf, t)
-            bad += int(G.as_unsigned(v)[0] != got[i])
-            checked += 1
-    return (f"consistent ({checked} payloads across all {world} shares recomputed on rank 0)" if bad == 0
-            else f"MISMATCH {bad}/{checked} across shards")
+        firsts, counts = [0], [count0]
+    if layout == "messages":  # two pieces per message; the payload piece is the odd one
+        firsts, counts = [2 * f for f in firsts], [2 * c for c in counts]
+    idx = [f for f, c in zip(firsts, counts) if c] + [f + c - 1 for f, c in zip(firsts, counts) if c]
+    return sorted(set(idx))
+
+
+def pmc_traffic(config, world, alg_bytes):
+    """roofline.traffic: HBM bytes per launch cannot be counted inside this
+    process -- they come from the committed rocprofv3 FETCH_SIZE / WRITE_SIZE
+    passes of this config (tools/gpu_r03.sh PART=pmc ->
+    profiles/pmc_traffic_<config>.json).  At N > 1 the profile (one GPU, the
+    whole batch) is scaled to rank 0's share by its traffic/algorithmic
+    ratio.  (None, reason) when there is no profile."""
+    rel = f"profiles/pmc_traffic_{config}.json"
+    path = os.path.join(ROOT, rel)
+    if not os.path.exists(path):
+        return None, f"no committed PMC profile for {config} ({rel})"
+    try:
+        prof = json.load(open(path))
+        if world == 1:
+            return prof["hbm_bytes_per_launch"], (f"{rel} (rocprofv3 FETCH_SIZE + WRITE_SIZE passes of this config, "
+                                                  "committed; not measured in this run)")
+        ratio = float(prof["hbm_bytes_per_launch"]) / float(prof["algorithmic_bytes_per_launch"])
+        return round(ratio * alg_bytes), (f"rank 0's share: its algorithmic bytes x {ratio:.5f}, the "
+                                          f"traffic/algorithmic ratio of {rel} (one GPU, whole batch, rocprofv3 "
+                                          "PMC passes, committed); not measured in this run")
+    except (OSError, ValueError, KeyError, ZeroDivisionError) as e:
+        return None, f"{rel} unreadable: {e}"
 
 
 if __name__ == "__main__":

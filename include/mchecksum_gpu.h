@@ -27,14 +27,17 @@
  * Streams: `stream` is a hipStream_t (NULL = the default stream).  Calls are
  * asynchronous and capture-safe once mchecksum_gpu_prepare() has run for the
  * method on the current device (it uploads the lookup tables).  Large batches
- * balance their payloads through a device-side work-queue slot of their
- * stream's own (up to 2048 streams per device; launches on one stream never
- * overlap).  Calls captured into a hipGraph, calls on hipStreamPerThread and
- * streams past the 2048th take a static split of the batch instead: a graph
- * replays its captured arguments, possibly on two execs at once, so no slot
- * could be exclusive to it.  The slot is keyed by the stream handle: a stream
- * destroyed with calls still in flight must be synchronized first if a new
- * stream may receive the same handle (its launches would share the slot).
+ * balance their payloads through a device-side slot of their stream's own: a
+ * work queue, or for mid-sized fixed batches a split re-weighted from the
+ * previous launch's per-XCD times (launches on one stream never overlap).
+ * (A handle names a new stream only after hipStreamDestroy of the old one,
+ * which returns once that stream's work has completed, so a reused handle
+ * never shares its slot with launches in flight.)  A device has 2048 slots; once all are owned,
+ * a new stream takes over the least recently used slot whose launches have
+ * all completed.  Calls captured into a hipGraph, calls on hipStreamPerThread
+ * and streams that find no idle slot take a plain static split of the batch
+ * instead: a graph replays its captured arguments, possibly on two execs at
+ * once, so no slot could be exclusive to it.
  *
  * Fail closed: every wait in the work queue is bounded.  A launch in which a
  * wait gives up (a protocol fault; 0 in every test run) adds 1 to the error
@@ -231,6 +234,21 @@ mchecksum_gpu_last_error(void);
  * Returns -1 without a usable device. */
 MCHECKSUM_PUBLIC long long
 mchecksum_gpu_queue_faults(void);
+
+/* Diagnostics: work-queue slot bookkeeping of the current device since the
+ * library was loaded, written to stats[0 .. min(n, MCHECKSUM_GPU_QSTAT_COUNT)):
+ * launches given a slot, launches that took the plain static split without
+ * one (graph captures, MCHECKSUM_GPU_BAL=0, no idle slot), slots that changed
+ * owner stream, busy slots passed over while looking for one, and streams
+ * that currently own a slot.  Host-side counters only: no device sync. */
+#define MCHECKSUM_GPU_QSTAT_SLOT 0
+#define MCHECKSUM_GPU_QSTAT_NOSLOT 1
+#define MCHECKSUM_GPU_QSTAT_RECLAIM 2
+#define MCHECKSUM_GPU_QSTAT_BUSY_SKIP 3
+#define MCHECKSUM_GPU_QSTAT_OWNERS 4
+#define MCHECKSUM_GPU_QSTAT_COUNT 5
+MCHECKSUM_PUBLIC int
+mchecksum_gpu_queue_stats(long long *stats, size_t n);
 
 #ifdef __cplusplus
 }

@@ -23,7 +23,8 @@ GPU_SYMBOLS = ("mchecksum_gpu_available", "mchecksum_gpu_prepare", "mchecksum_gp
                "mchecksum_gpu_checksum_offsets", "mchecksum_gpu_verify_offsets", "mchecksum_gpu_verify_messages",
                "mchecksum_gpu_lanes_per_payload", "mchecksum_gpu_last_error", "mchecksum_gpu_segments_work_size",
                "mchecksum_gpu_checksum_segments", "mchecksum_gpu_verify_core_headers",
-               "mchecksum_gpu_queue_faults", "mchecksum_gpu_set_error_word", "mchecksum_gpu_checksum_xdr")
+               "mchecksum_gpu_queue_faults", "mchecksum_gpu_set_error_word", "mchecksum_gpu_checksum_xdr",
+               "mchecksum_gpu_queue_stats")
 CORE_HEADER_REQUEST, CORE_HEADER_RESPONSE = 0, 1
 # XDR schema field kinds (include/mchecksum_gpu.h)
 XDR_INT, XDR_OPAQUE, XDR_OPAQUE_LEN, XDR_RAW, XDR_RAW_LEN, XDR_SKIP_IF_ZERO = 0, 1, 2, 3, 4, 5
@@ -86,6 +87,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     L.mchecksum_gpu_last_error.restype = c_char_p
     L.mchecksum_gpu_queue_faults.argtypes = []
     L.mchecksum_gpu_queue_faults.restype = ctypes.c_longlong
+    L.mchecksum_gpu_queue_stats.argtypes = [c_void_p, c_size_t]
+    L.mchecksum_gpu_queue_stats.restype = c_int
     L.mchecksum_gpu_set_error_word.argtypes = [c_void_p]
     L.mchecksum_gpu_set_error_word.restype = c_int
     L.mchecksum_gpu_checksum_xdr.argtypes = [c_char_p, ctypes.POINTER(XdrField), c_size_t, c_void_p, c_void_p,

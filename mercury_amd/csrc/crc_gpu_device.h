@@ -170,6 +170,10 @@ struct BatchArgs {
     // MSB-first model on a verify call: the kernel's value is the CRC
     // byte-swapped (crc_gpu_layout.h), so swap before comparing
     uint32_t bswap;
+    // feedback-balanced static split (BalBank below): the slot's two banks
+    // and this launch's sequence number on them; nullptr = plain split
+    struct BalBank *bal;
+    uint32_t bal_seq;
 };
 // Piece size of a split payload: 256 KiB = 256 steps of the G = 64 loop.
 constexpr uint64_t kSplitBytes = 256u << 10;
@@ -199,7 +203,10 @@ constexpr uint64_t kSplitBytes = 256u << 10;
 // runs the same protocol on the CPU under random interleavings.
 // Slot layout (one counter per 256-B line): [0, 8) sub-queue tickets,
 // [8, 16) exited workgroups per group (blockIdx % 8), [16] exited groups,
-// [17] fault flag of the launch.
+// [17] fault flag of the launch -- all zeroed by the launch's last group --
+// and [18] the number of launches completed on the slot (never zeroed: the
+// host compares it with the launches it issued before it gives the slot to
+// another stream, mchecksum_gpu.hip queue_slot).
 //
 // Exclusivity.  A slot serves one launch at a time: the host hands the queue
 // only to eager launches, each on a slot of its stream's own (launches on one
@@ -218,8 +225,9 @@ constexpr uint32_t kQStride = 32;  // u64 words between counters
 constexpr uint32_t kQGroupDone = kQSub;
 constexpr uint32_t kQAllDone = 2 * kQSub;
 constexpr uint32_t kQFault = 2 * kQSub + 1;
-constexpr uint32_t kQSlotLines = 2 * kQSub + 2;
-constexpr uint32_t kQSlotWords = kQSlotLines * kQStride;
+constexpr uint32_t kQSlotLines = 2 * kQSub + 2;  // lines a launch leaves zeroed
+constexpr uint32_t kQDone = kQSlotLines;
+constexpr uint32_t kQSlotWords = (kQSlotLines + 1) * kQStride;
 // Chunk size: a power of two, about a quarter of a workgroup's fair share
 // of units, between 1 and 32 (C4: 32 units; a 5000-payload batch: 4).
 // Fixed 16 starved half the workgroups of C3's 8192 units at 2 WGs per CU; 32
@@ -400,6 +408,205 @@ __device__ __attribute__((unused)) void wg_queue_init(WgQueue *L, unsigned long 
     (void)wg_publish(L, 0, wg_fetch(L, q, plan.nch), plan.cl);
 }
 
+// ------------------------------------------------ balanced static split --
+// The plain static split (units wave, wave + #waves, ...) ends when the
+// slowest XCD ends: the per-XCD mean end of C2's waves spans 33.0-40.5 us
+// (profiles/r02/tail_trace_c2_static.json), and the work queue that would
+// balance it costs more per chunk fetch than it saves on a 44 us launch
+// (profiles/r02/ab_queue_chunks_c2.log).  Feedback instead: every launch on a
+// slot records, per workgroup, its entry stamp and the exit stamp of its last
+// wave; the next launch on the slot turns them into the time each group of
+// workgroups (blockIdx % 8, the XCD dispatch order) took for its share and
+// apportions its own units in proportion to the groups' measured rates (an
+// EMA over launches).  Nothing goes through the host and nothing waits
+// inside a launch.  Every workgroup computes the same shares from the same
+// record -- the previous launch on the slot has completed and launches on a
+// slot never overlap (queue_slot, mchecksum_gpu.hip) -- so the split is
+// exact: every unit exactly once, whatever the weights.  Two banks: launch s
+// reads bank s & 1 and writes bank (s + 1) & 1.
+//
+// Units go out in rounds of MCK_BAL_ROUND x #waves: round r gives group g
+// the units [base + c_g, base + c_(g+1)), c = the cumulative weights scaled
+// to the round, and the group's waves stride over them -- every XCD stays in
+// the same moving window of the batch, as with the plain split.
+#ifndef MCK_BAL
+#define MCK_BAL 1
+#endif
+#ifndef MCK_BAL64
+#define MCK_BAL64 0
+#endif
+#ifndef MCK_BAL_ROUND
+#define MCK_BAL_ROUND 1
+#endif
+#ifndef MCK_BAL_ALPHA
+#define MCK_BAL_ALPHA 0.5f
+#endif
+constexpr uint32_t kBalGroups = kQSub;
+constexpr uint32_t kBalMaxWg = 512;
+constexpr uint32_t kBalOne = 1u << 24;  // weights are fixed point, summing to kBalOne
+struct BalBank {
+    uint32_t grid;           // workgroups of the launch that wrote this bank (0: none yet)
+    uint32_t w[kBalGroups];  // the group weights that launch used
+    uint32_t pad[7];
+    unsigned long long rec[2 * kBalMaxWg];  // per workgroup: entry stamp, exit stamp of its last wave
+};
+struct BalLds {
+    uint32_t cut[kBalGroups + 1];  // cumulative weights of this launch
+    uint32_t span[kBalGroups];     // the previous launch's time per group (100 MHz ticks)
+    uint32_t hdr[1 + kBalGroups];  // the previous launch's grid and weights
+    uint32_t exited;
+    unsigned long long start;
+};
+
+template <typename T>
+__device__ __forceinline__ T wave_max(T v) {
+#pragma unroll
+    for (int k = 1; k < 64; k <<= 1) {
+        const T o = __shfl_xor(v, k, 64);
+        v = o > v ? o : v;
+    }
+    return v;
+}
+template <typename T>
+__device__ __forceinline__ T wave_min(T v) {
+#pragma unroll
+    for (int k = 1; k < 64; k <<= 1) {
+        const T o = __shfl_xor(v, k, 64);
+        v = o < v ? o : v;
+    }
+    return v;
+}
+
+// What a lane loads of the previous launch's bank before the LDS fill, so the
+// loads' latency hides under the fill: wave g < 8 the records of workgroups
+// g, g + 8, ... (all 512 -- which of them the launch had is only known from
+// the header, so masking waits until after the fill); wave 8 the header.
+struct BalPre {
+    unsigned long long s, e;
+    uint32_t h;
+};
+
+__device__ __forceinline__ BalPre bal_prefetch(const BatchArgs &a, BalLds *bl) {
+    const uint32_t wib = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const BalBank *pb = a.bal + (a.bal_seq & 1u);
+    BalPre p{~0ull, 0ull, 0u};
+    if (threadIdx.x == 0) {
+        bl->start = wall_clock64();
+        bl->exited = 0;
+    }
+    if (wib < kBalGroups) {
+        const uint32_t j = wib + kBalGroups * lane;  // < kBalMaxWg
+        p.s = pb->rec[2 * j];
+        p.e = pb->rec[2 * j + 1];
+    } else if (wib == kBalGroups && lane <= kBalGroups) {
+        p.h = lane == 0 ? pb->grid : pb->w[lane - 1];
+    }
+    return p;
+}
+
+// After the fill, before its barrier: wave 8 stores the header; waves
+// g < 8 keep their records in registers for bal_span (after the barrier,
+// when the header's grid is known in LDS).
+__device__ __forceinline__ void bal_stash(BalLds *bl, const BalPre &p) {
+    const uint32_t wib = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    if (wib == kBalGroups && lane <= kBalGroups) bl->hdr[lane] = p.h;
+}
+
+// After the fill barrier: wave g reduces group g's records (of workgroups the
+// previous launch had) to the group's time span; then thread 0 of every
+// workgroup turns spans and weights into this launch's cuts (identical inputs
+// -> identical cuts), workgroup 0 records the weights for the next launch.
+// Two barriers.
+__device__ __forceinline__ void bal_plan(const BatchArgs &a, BalLds *bl, const BalPre &p) {
+    const uint32_t wib = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const uint32_t grid = bl->hdr[0];
+    if (wib < kBalGroups) {
+        const bool live = grid <= kBalMaxWg && wib + kBalGroups * lane < grid;
+        const unsigned long long s = wave_min(live ? p.s : ~0ull), e = wave_max(live ? p.e : 0ull);
+        if (lane == 0) bl->span[wib] = e > s && e - s < (1ull << 31) ? (uint32_t)(e - s) : 0u;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t w[kBalGroups];
+        uint32_t sum = 0;
+        bool ok = grid >= kBalGroups && grid <= kBalMaxWg;
+#pragma unroll
+        for (uint32_t g = 0; g < kBalGroups; g++) {
+            sum += bl->hdr[1 + g];
+            ok = ok && bl->hdr[1 + g] > 0 && bl->span[g] > 0;
+        }
+        ok = ok && sum == kBalOne;
+        if (!ok) {
+#pragma unroll
+            for (uint32_t g = 0; g < kBalGroups; g++) w[g] = kBalOne / kBalGroups;
+        } else {
+            // rate of group g = its share / its time; move the weights by
+            // MCK_BAL_ALPHA towards the rate-proportional split
+            float r[kBalGroups], rs = 0.f, v[kBalGroups], vs = 0.f;
+#pragma unroll
+            for (uint32_t g = 0; g < kBalGroups; g++) {
+                r[g] = (float)bl->hdr[1 + g] / (float)bl->span[g];
+                rs += r[g];
+            }
+#pragma unroll
+            for (uint32_t g = 0; g < kBalGroups; g++) {
+                float x = (1.f - MCK_BAL_ALPHA) * (float)bl->hdr[1 + g] + MCK_BAL_ALPHA * (float)kBalOne * (r[g] / rs);
+                x = x < (float)(kBalOne / 32) ? (float)(kBalOne / 32) : x > (float)(kBalOne / 2) ? (float)(kBalOne / 2) : x;
+                v[g] = x;
+                vs += x;
+            }
+            uint32_t acc = 0;
+#pragma unroll
+            for (uint32_t g = 0; g + 1 < kBalGroups; g++) {
+                w[g] = (uint32_t)(v[g] / vs * (float)kBalOne);
+                acc += w[g];
+            }
+            w[kBalGroups - 1] = kBalOne - acc;
+        }
+        bl->cut[0] = 0;
+#pragma unroll
+        for (uint32_t g = 0; g < kBalGroups; g++) bl->cut[g + 1] = bl->cut[g] + w[g];
+        if (blockIdx.x == 0) {
+            BalBank *ob = a.bal + ((a.bal_seq + 1) & 1u);
+            ob->grid = gridDim.x;
+#pragma unroll
+            for (uint32_t g = 0; g < kBalGroups; g++) ob->w[g] = w[g];
+        }
+    }
+    __syncthreads();
+}
+
+// Exit counting of a launch that holds a slot, run by every wave once it has
+// no more units (wave-uniform).  One global atomic per wave on a single line
+// serialised ~4096 x 45 ns at the end of every launch (C2 ran 2x slower), so
+// it is hierarchical: waves count in LDS (*wg_exited), the last wave of a
+// workgroup runs wg_last() and counts in its group's line, the last workgroup
+// of a group in the slot's line; the last group zeroes the slot's protocol
+// lines for the next launch and then, after a fence, counts the launch done.
+template <class F>
+__device__ __forceinline__ void slot_exit(unsigned long long *queue, uint32_t *wg_exited, F &&wg_last) {
+    const bool l0 = (threadIdx.x & 63u) == 0;
+    uint32_t wl = 0;
+    if (l0) wl = atomicAdd(wg_exited, 1u) == blockDim.x / 64u - 1u;
+    uint32_t last = 0;
+    if (__builtin_amdgcn_readfirstlane(wl)) {
+        wg_last();
+        if (l0) {
+            const uint32_t g = blockIdx.x % kQSub;
+            const uint32_t wgs = (gridDim.x - g + kQSub - 1) / kQSub;  // workgroups in group g
+            const uint32_t groups = gridDim.x < kQSub ? gridDim.x : kQSub;
+            last = atomicAdd(queue + (kQGroupDone + g) * kQStride, 1ull) == wgs - 1ull &&
+                   atomicAdd(queue + kQAllDone * kQStride, 1ull) == groups - 1ull;
+        }
+    }
+    if (__builtin_amdgcn_readfirstlane(last)) {  // one instruction: lane j zeroes line j
+        const uint32_t j = threadIdx.x & 63u;
+        if (j < kQSlotLines) atomicExch(queue + j * kQStride, 0ull);
+        __threadfence();
+        if (j == 0) atomicAdd(queue + kQDone * kQStride, 1ull);
+    }
+}
+
 // Calls body(u) for this wave's units: through the work queue (DYN: the
 // throughput kernels, wg_queue_init has run) or u = wave, wave + nw, ... (the
 // light layout's small batches, and DYN launches without a slot).
@@ -415,7 +622,7 @@ __device__ __attribute__((unused)) void wg_queue_init(WgQueue *L, unsigned long 
 #endif
 template <bool DYN, class F>
 __device__ __forceinline__ bool for_each_unit(WgQueue *L, unsigned long long *queue, uint64_t n, uint32_t wave,
-                                              uint32_t nw, F &&body) {
+                                              uint32_t nw, F &&body, const BalLds *bl = nullptr) {
     if constexpr (DYN) {
         // One call site of body for both splits: a second inlined copy of the
         // payload loop made the offsets kernels spill, and so does the copy
@@ -531,30 +738,61 @@ __device__ __forceinline__ bool for_each_unit(WgQueue *L, unsigned long long *qu
         // (before its own exit is counted, so the slot cannot be released yet).
         uint32_t first = 0;
         if (l0 && flt) first = atomicCAS(queue + kQFault * kQStride, 0ull, 1ull) == 0ull;
-        // Exit counting is hierarchical: one global atomic per wave on a
-        // single line serialised ~4096 x 45 ns at the end of every launch
-        // (C2 ran 2x slower).  Waves count in LDS, the last wave of a
-        // workgroup counts in its group's line, the last workgroup of a group
-        // in the slot's line; the last group zeroes the slot for the next
-        // launch on this stream.
-        uint32_t last = 0;
-        if (l0 && atomicAdd(&L->exited, 1u) == blockDim.x / 64u - 1u) {
-            const uint32_t g = blockIdx.x % kQSub;
-            const uint32_t wgs = (gridDim.x - g + kQSub - 1) / kQSub;  // workgroups in group g
-            const uint32_t groups = gridDim.x < kQSub ? gridDim.x : kQSub;
-            last = atomicAdd(queue + (kQGroupDone + g) * kQStride, 1ull) == wgs - 1ull &&
-                   atomicAdd(queue + kQAllDone * kQStride, 1ull) == groups - 1ull;
-        }
-        if (__builtin_amdgcn_readfirstlane(last)) {  // one instruction: lane j zeroes line j
-            const uint32_t j = threadIdx.x & 63u;
-            if (j < kQSlotLines) atomicExch(queue + j * kQStride, 0ull);
-        }
+        slot_exit(queue, &L->exited, [] {});
         (void)nw;
         return __builtin_amdgcn_readfirstlane(first) != 0;
     } else {
-        for (uint64_t u = wave; u < n; u += nw) body(u);
+        // plain split: u = wave, wave + nw, ...; balanced (bl): see above.
+        // One call site of body for both.
+        (void)L;
+        (void)queue;
+        const uint32_t g = blockIdx.x % kBalGroups, wpb = blockDim.x / 64u;
+        const uint32_t nwg = (gridDim.x - g + kBalGroups - 1) / kBalGroups * wpb;  // waves of group g
+        const uint32_t lw = (blockIdx.x / kBalGroups) * wpb + (threadIdx.x >> 6);
+        const uint64_t S = (uint64_t)MCK_BAL_ROUND * nw;
+        const uint32_t c0 = bl ? __builtin_amdgcn_readfirstlane(bl->cut[g]) : 0u;
+        const uint32_t c1 = bl ? __builtin_amdgcn_readfirstlane(bl->cut[g + 1]) : 0u;
+        // group g's units, concatenated over the rounds, go to its waves in
+        // turn: wave lw takes the group's units lw, lw + nwg, ... -- so a
+        // share that is not a multiple of the group's waves spreads its surplus
+        // over all waves instead of piling it on the first few of every round.
+        // k indexes the group's units from the round at `base` on ([lo, hi)).
+        uint64_t base = 0, lo = 0, hi = n, k = lw;
+        auto settle = [&]() -> uint64_t {
+            for (; base < n; base += S) {
+                const uint64_t size = n - base < S ? n - base : S;
+                lo = base + ((size * c0) >> 24);
+                hi = base + ((size * c1) >> 24);
+                if (k < hi - lo) return lo + k;
+                k -= hi - lo;
+            }
+            return n;
+        };
+        uint64_t u = bl ? settle() : wave;
+        while (u < n) {
+            body(u);
+            if (bl) {
+                k = u - lo + nwg;
+                u = settle();
+            } else {
+                u += nw;
+            }
+        }
         return false;
     }
+}
+
+// After a balanced launch's units (every wave): exit counting on the slot;
+// the last wave of each workgroup records the workgroup's entry and exit
+// stamps for the next launch.
+__device__ __forceinline__ void bal_exit(const BatchArgs &a, BalLds *bl) {
+    slot_exit(a.queue, &bl->exited, [&] {
+        if ((threadIdx.x & 63u) == 0 && blockIdx.x < kBalMaxWg) {
+            BalBank *ob = a.bal + ((a.bal_seq + 1) & 1u);
+            ob->rec[2 * blockIdx.x] = bl->start;
+            ob->rec[2 * blockIdx.x + 1] = wall_clock64();
+        }
+    });
 }
 
 // Run by the wave for_each_unit picked after a give-up (wave-uniform): the
@@ -858,16 +1096,6 @@ __device__ __forceinline__ uint32_t payload32_aligned(TAB lds, const uint8_t *p,
 }
 #endif
 
-template <typename T>
-__device__ __forceinline__ T wave_max(T v) {
-#pragma unroll
-    for (int k = 1; k < 64; k <<= 1) {
-        const T o = __shfl_xor(v, k, 64);
-        v = o > v ? o : v;
-    }
-    return v;
-}
-
 // Any alignment, any length (0 included).  Per-lane window; the wave loops to
 // the largest step count of its groups.
 template <int LOG2G, bool NT, class TAB>
@@ -1032,8 +1260,20 @@ __device__ __forceinline__ void wave_range(const uint64_t *off, uint64_t count, 
 #if MCK_TRACE
 constexpr int kTraceWaves = 16384;
 __device__ unsigned long long g_mck_trace[3 * kTraceWaves];
-#define MCK_STAMP(w, k) \
-    do { if ((threadIdx.x & 63u) == 0 && (w) < kTraceWaves) g_mck_trace[3 * (w) + (k)] = wall_clock64(); } while (0)
+// the XCD each wave ran on (hardware register XCC_ID), stamped at entry
+__device__ unsigned int g_mck_trace_xcc[kTraceWaves];
+__device__ __forceinline__ unsigned int xcc_id() {
+    unsigned int r;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(r));
+    return r & 15u;
+}
+#define MCK_STAMP(w, k)                                                                   \
+    do {                                                                                  \
+        if ((threadIdx.x & 63u) == 0 && (w) < kTraceWaves) {                              \
+            g_mck_trace[3 * (w) + (k)] = wall_clock64();                                  \
+            if ((k) == 0) g_mck_trace_xcc[(w)] = xcc_id();                                \
+        }                                                                                 \
+    } while (0)
 #else
 #define MCK_STAMP(w, k) do { } while (0)
 #endif
@@ -1070,8 +1310,17 @@ __global__ __launch_bounds__(kBlk32<LIGHT>, 1) void crc32c_batch_kernel(BatchArg
     if (!DYN) return;  // diagnostic: launch cost alone
 #endif
     if (DYN && threadIdx.x == 0) wg_queue_init(&wgq, a.queue, units);
+    // feedback-balanced static split (the host passes a record only for
+    // eager launches with a slot, >= 8 and <= kBalMaxWg workgroups)
+    constexpr bool kBal = MCK_BAL && !DYN && !LIGHT && MODE == kFixedAligned;
+    __shared__ BalLds bl;
+    const bool bal = kBal && a.bal != nullptr;
+    BalPre bp{};
+    if (bal) bp = bal_prefetch(a, &bl);
     fill_lds32<LIGHT, kBlk32<LIGHT>>(lds_raw, pk);
+    if (bal) bal_stash(&bl, bp);
     __syncthreads();
+    if (bal) bal_plan(a, &bl, bp);
 #if defined(MCK_EMPTY) && MCK_EMPTY == 1
     if (!DYN) return;  // diagnostic: launch + LDS table fill
 #endif
@@ -1124,8 +1373,9 @@ __global__ __launch_bounds__(kBlk32<LIGHT>, 1) void crc32c_batch_kernel(BatchArg
         else
             x = payload32_generic<LOG2G, NT>(lds, pk, a.base + pc * a.stride, a.len, gl, lc0, lc1);
         if (act && gl == 0) emit<uint32_t, VERIFY>(a, p, x ^ xorout);
-    });
+    }, bal ? &bl : nullptr);
     if (faulted) fail_closed<VERIFY>(a);
+    if (bal) bal_exit(a, &bl);
     MCK_STAMP(wave, 2);
 }
 
@@ -1592,8 +1842,17 @@ __global__ __launch_bounds__(kBlk64<MODE>, kWpe64<MODE>) void crc64_batch_kernel
     constexpr bool DYN = dyn_policy(64, MODE, NT, false) || SPLIT;
     MCK_STAMP(blockIdx.x * kWPB + (threadIdx.x >> 6), 0);
     if (DYN && threadIdx.x == 0) wg_queue_init(&wgq, a.queue, units);
+    // (off by default: the split's state pushed the 64-VGPR static CRC-64
+    // kernels into 13-18 VGPR spills)
+    constexpr bool kBal = MCK_BAL && MCK_BAL64 && !DYN && MODE == kFixedAligned;
+    __shared__ BalLds bl;
+    const bool bal = kBal && a.bal != nullptr;
+    BalPre bp{};
+    if (bal) bp = bal_prefetch(a, &bl);
     fill_lds64<S::block, S::ops_mode>(lds, pk);
+    if (bal) bal_stash(&bl, bp);
     __syncthreads();
+    if (bal) bal_plan(a, &bl, bp);
     MCK_STAMP(blockIdx.x * kWPB + (threadIdx.x >> 6), 1);
 
     const uint32_t lane = threadIdx.x & 63u;
@@ -1648,8 +1907,9 @@ __global__ __launch_bounds__(kBlk64<MODE>, kWpe64<MODE>) void crc64_batch_kernel
         else
             x = payload64_generic<LOG2G, NT>(lds, pk, a.base + pc * a.stride, a.len, gl, lc);
         if (act && gl == 0) emit<uint64_t, VERIFY>(a, p, x ^ xorout);
-    });
+    }, bal ? &bl : nullptr);
     if (faulted) fail_closed<VERIFY>(a);
+    if (bal) bal_exit(a, &bl);
     MCK_STAMP(blockIdx.x * kWPB + (threadIdx.x >> 6), 2);
 }
 

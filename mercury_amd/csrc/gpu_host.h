@@ -17,6 +17,20 @@ namespace mck {
 
 constexpr int kMaxDev = 64;
 
+constexpr uint32_t kStreamSlots = 2048;
+constexpr uint32_t kQueueSlots = kStreamSlots;
+
+// One slot: the work-queue counters (kQSlotWords words in DevCtx::queue) and
+// the balanced split's record (two BalBanks in DevCtx::bal), owned by one
+// stream at a time.
+struct SlotState {
+    uintptr_t sid = 0;  // owning stream (handle)
+    uint64_t issued = 0;         // launches handed this slot (the kernels count completions, kQDone)
+    uint64_t last_use = 0;       // LRU tick
+    uint32_t bal_seq = 0;        // balanced launches on the slot (bank parity)
+    bool owned = false;
+};
+
 struct DevCtx {
     bool init = false;
     int cus = 0;
@@ -24,15 +38,31 @@ struct DevCtx {
     void *ext[MCK_NMODELS] = {};  // mchecksum_gpu_ext.hip's per-model tables
     // Work-queue slots of the batch kernels (WgQueue, crc_gpu_device.h):
     // kQueueSlots zeroed counter sets; a launch's last group re-zeroes its slot.
-    // Eager launches use a slot of their stream's own (the first kStreamSlots
-    // streams seen on the device; launches on one stream never overlap).
-    // Graph-captured launches and streams past the table get none and take
-    // the static split (crc_gpu_device.h, "Exclusivity").
+    // Eager launches use a slot of their stream's own (keyed by the handle);
+    // launches on one stream never overlap.  When all slots are owned, the
+    // least recently used slot whose issued launches have all completed
+    // (kQDone) changes owner.
+    // Graph-captured launches, and streams that find no idle slot, get none
+    // and take the plain static split (crc_gpu_device.h, "Exclusivity").
     unsigned long long *queue = nullptr;
-    std::unordered_map<void *, uint32_t> stream_slot;  // guarded by g_mu
+    void *bal = nullptr;                        // kQueueSlots x 2 BalBanks
+    SlotState slot[kQueueSlots];               // guarded by g_mu
+    std::unordered_map<uintptr_t, uint32_t> sid_slot;  // guarded by g_mu
+    uint32_t nslots = 0;                        // slots handed out so far
+    uint64_t tick = 0;
+    hipStream_t probe = nullptr;                // private stream: reads kQDone words
+    unsigned long long *probe_host = nullptr;   // pinned word for those reads
+    // diagnostics (mchecksum_gpu_queue_stats)
+    long long n_slot = 0, n_noslot = 0, n_reclaim = 0, n_busy_skip = 0;
 };
-constexpr uint32_t kStreamSlots = 2048;
-constexpr uint32_t kQueueSlots = kStreamSlots;
+
+// A launch's slot: counters, balance record and its sequence on that record.
+struct SlotRef {
+    unsigned long long *q = nullptr;
+    void *bal = nullptr;  // the slot's two BalBanks (crc_gpu_device.h)
+    uint32_t seq = 0;
+    int idx = -1;
+};
 
 extern std::mutex g_mu;
 
@@ -56,9 +86,16 @@ int prologue(const char *method, int log2g, int *width, DevCtx **c, const void *
 // (caller holds g_mu).
 int get_ext(DevCtx *c, int idx, const void **out);
 // Work-queue slot for one launch of a throughput (non-light) batch kernel on
-// `stream`, exclusive to that stream; nullptr (static split) for a launch
-// being captured into a graph or a stream past the table.
-unsigned long long *queue_slot(DevCtx *c, void *stream);
+// `stream`, exclusive to that stream; empty (static split) for a launch being
+// captured into a graph or a stream that finds no idle slot.  `bal`: the
+// launch uses the balance record (takes a sequence number on it).  Every
+// launch given a slot must count itself done on it (slot_exit): if the launch
+// fails to start, slot_unissue() takes the launch back.
+SlotRef queue_slot(DevCtx *c, void *stream, bool bal = false);
+void slot_unissue(DevCtx *c, const SlotRef &r);
+// Queue-fault count of mchecksum_gpu_ext.hip's kernels (their own copy of
+// g_mck_queue_faults) on the current device; -1 on error.
+long long ext_queue_faults();
 // This host thread's fail-closed report word (mchecksum_gpu_set_error_word), or nullptr.
 uint32_t *error_word();
 

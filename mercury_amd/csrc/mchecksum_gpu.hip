@@ -128,11 +128,20 @@ int device_ctx(DevCtx **out) {
         if (e != hipSuccess) return hip_err(e, "hipDeviceGetAttribute");
         c.cus = cus > 0 ? cus : 1;
         const size_t qbytes = (size_t)kQueueSlots * kQSlotWords * sizeof(unsigned long long);
+        const size_t bbytes = (size_t)kQueueSlots * 2 * sizeof(BalBank);
         e = hipMalloc(reinterpret_cast<void **>(&c.queue), qbytes);
         if (e == hipSuccess) e = hipMemset(c.queue, 0, qbytes);
+        if (e == hipSuccess) e = hipMalloc(&c.bal, bbytes);
+        if (e == hipSuccess) e = hipMemset(c.bal, 0, bbytes);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&c.probe, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&c.probe_host), sizeof(unsigned long long));
         if (e != hipSuccess) {
             if (c.queue) (void)hipFree(c.queue);
+            if (c.bal) (void)hipFree(c.bal);
+            if (c.probe) (void)hipStreamDestroy(c.probe);
             c.queue = nullptr;
+            c.bal = nullptr;
+            c.probe = nullptr;
             return hip_err(e, "work-queue allocation");
         }
         c.init = true;
@@ -178,7 +187,27 @@ int get_pack(DevCtx *c, int idx, int log2g, const void **pack) {
     return 0;
 }
 
-unsigned long long *queue_slot(DevCtx *c, void *stream) {
+// Launches slot i has completed (its kernels' kQDone counter), read on the
+// private stream; -1 if the read fails (caller holds g_mu).
+long long slot_done(DevCtx *c, uint32_t i) {
+    if (hipMemcpyAsync(c->probe_host, c->queue + (size_t)i * kQSlotWords + kQDone * kQStride,
+                       sizeof(unsigned long long), hipMemcpyDeviceToHost, c->probe) != hipSuccess ||
+        hipStreamSynchronize(c->probe) != hipSuccess) {
+        (void)hipGetLastError();
+        return -1;
+    }
+    return (long long)*c->probe_host;
+}
+
+// Balanced split off (MCHECKSUM_GPU_BAL=0): every static launch takes the
+// plain split without a slot (A/B switch, read per call like the other knobs).
+bool bal_enabled() {
+    const char *env = getenv("MCHECKSUM_GPU_BAL");
+    return !(env && env[0] == '0');
+}
+
+SlotRef queue_slot(DevCtx *c, void *stream, bool bal) {
+    SlotRef r;
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing((hipStream_t)stream, &st) != hipSuccess) {
         (void)hipGetLastError();
@@ -187,16 +216,88 @@ unsigned long long *queue_slot(DevCtx *c, void *stream) {
     // A captured launch replays with these arguments, possibly on two graph
     // execs at once: no exclusive slot exists for it, so it takes the static
     // split (crc_gpu_device.h, "Exclusivity").
-    if (st != hipStreamCaptureStatusNone) return nullptr;
+    if (st != hipStreamCaptureStatusNone || (bal && !bal_enabled())) {
+        std::lock_guard<std::mutex> lk(g_mu);
+        c->n_noslot++;
+        return r;
+    }
     // hipStreamPerThread names a different stream in every host thread: one
     // slot for that handle could serve two launches at once
-    if ((hipStream_t)stream == hipStreamPerThread) return nullptr;
     std::lock_guard<std::mutex> lk(g_mu);
-    auto it = c->stream_slot.find(stream);
-    if (it == c->stream_slot.end() && c->stream_slot.size() < kStreamSlots)
-        it = c->stream_slot.emplace(stream, (uint32_t)c->stream_slot.size()).first;
-    // this stream's own slot (its launches never overlap), or none past the table
-    return it != c->stream_slot.end() ? c->queue + (size_t)it->second * kQSlotWords : nullptr;
+    if ((hipStream_t)stream == hipStreamPerThread) {
+        c->n_noslot++;
+        return r;
+    }
+    // Keyed by handle.  A handle names a new stream only after the old one was
+    // destroyed, and hipStreamDestroy returns once the stream's queued work has
+    // completed (measured: tests/test_gpu_queue.py, destroy with a launch in
+    // flight), so the new owner never overlaps the old owner's launches.
+    const uintptr_t sid = reinterpret_cast<uintptr_t>(stream);
+    uint32_t i;
+    auto it = c->sid_slot.find(sid);
+    if (it != c->sid_slot.end()) {
+        i = it->second;  // this stream's own slot: its launches never overlap
+    } else if (c->nslots < kQueueSlots) {
+        i = c->nslots++;
+    } else {
+        // All slots owned: the least recently used ones, oldest first, until
+        // one has completed every launch it was issued (a destroyed stream's
+        // work may still be in flight).  None idle among the oldest 8: this
+        // launch takes the static split.
+        uint32_t cand[8];
+        uint64_t ct[8];
+        uint32_t nc = 0;
+        for (uint32_t k = 0; k < kQueueSlots; k++) {
+            const uint64_t t = c->slot[k].last_use;
+            uint32_t pos = nc < 8 ? nc++ : 8;
+            if (pos == 8) {
+                if (t >= ct[7]) continue;
+                pos = 7;
+            }
+            while (pos > 0 && ct[pos - 1] > t) {
+                ct[pos] = ct[pos - 1];
+                cand[pos] = cand[pos - 1];
+                pos--;
+            }
+            ct[pos] = t;
+            cand[pos] = k;
+        }
+        i = kQueueSlots;
+        for (uint32_t k = 0; k < nc && i == kQueueSlots; k++) {
+            if (slot_done(c, cand[k]) == (long long)c->slot[cand[k]].issued) i = cand[k];
+            else c->n_busy_skip++;
+        }
+        if (i == kQueueSlots) {
+            c->n_noslot++;
+            return r;
+        }
+        c->sid_slot.erase(c->slot[i].sid);
+        c->n_reclaim++;
+    }
+    SlotState &s = c->slot[i];
+    if (!s.owned || s.sid != sid) {
+        s.owned = true;
+        s.sid = sid;
+        c->sid_slot[sid] = i;
+    }
+    s.issued++;
+    s.last_use = ++c->tick;
+    c->n_slot++;
+    r.q = c->queue + (size_t)i * kQSlotWords;
+    r.idx = (int)i;
+    if (bal) {
+        r.bal = static_cast<BalBank *>(c->bal) + 2 * (size_t)i;
+        r.seq = s.bal_seq++;
+    }
+    return r;
+}
+
+void slot_unissue(DevCtx *c, const SlotRef &r) {
+    if (r.idx < 0) return;
+    std::lock_guard<std::mutex> lk(g_mu);
+    SlotState &s = c->slot[r.idx];
+    s.issued--;
+    if (r.bal) s.bal_seq--;
 }
 
 uint32_t *error_word() { return t_err_word; }
@@ -363,8 +464,11 @@ int do_offsets(const char *method, const void *base, const uint64_t *offsets, si
     else
         k = verify ? (nt ? kernel_ptr<64, 6, kOffsets, true, true>() : kernel_ptr<64, 6, kOffsets, true>())
                    : (nt ? kernel_ptr<64, 6, kOffsets, false, true>() : kernel_ptr<64, 6, kOffsets, false>());
-    if (dyn_policy(width, kOffsets, nt, light)) a.queue = queue_slot(c, stream);
+    SlotRef sr;
+    if (dyn_policy(width, kOffsets, nt, light)) sr = queue_slot(c, stream);
+    a.queue = sr.q;
     rc = launch(k, a, grid_for(c, count, k), stream);
+    if (rc != MCHECKSUM_GPU_OK) slot_unissue(c, sr);
     if (rc == MCHECKSUM_GPU_OK && gpu_msb(midx) && !verify) rc = swap_outputs(out, count, width, stream);
     return rc;
 }
@@ -412,7 +516,6 @@ int launch_fixed(DevCtx *c, int idx, const void *pack, int width, int lg, const 
         }
         a.shift = shift;
         a.split_log2 = sl;
-        a.queue = queue_slot(c, stream);
         // the pieces XOR their terms into out[]: zero it first, in stream order,
         // with a kernel -- a hipMemsetAsync captured into a graph did not order
         // against the kernel node on replays after the first (the pieces landed
@@ -427,22 +530,37 @@ int launch_fixed(DevCtx *c, int idx, const void *pack, int width, int lg, const 
                                        Shape<64, kFixedAligned>::blocks_per_cu}
                              : KLaunch{crc64_batch_kernel<6, kFixedAligned, false, false, true>, Shape<64, kFixedAligned>::block,
                                        Shape<64, kFixedAligned>::blocks_per_cu};
+        const SlotRef sr = queue_slot(c, stream);
+        a.queue = sr.q;
         int rc = launch(k, a, grid_for(c, (uint64_t)count << sl, k), stream);
+        if (rc != MCHECKSUM_GPU_OK) slot_unissue(c, sr);
         if (rc == MCHECKSUM_GPU_OK && gpu_msb(idx)) rc = swap_outputs(dev_out, count, width, stream);
         return rc;
     }
     const KLaunch k = width == 32 ? pick_fixed<32>(lg, aligned, nt, light) : pick_fixed<64>(lg, aligned, nt, false);
     const uint64_t ppw = 64u >> lg;
-    if (dyn_policy(width, aligned ? kFixedAligned : kFixedGeneric, nt, light)) a.queue = queue_slot(c, stream);
+    const bool dyn = dyn_policy(width, aligned ? kFixedAligned : kFixedGeneric, nt, light);
     const uint64_t units = (count + ppw - 1) / ppw;
     unsigned blocks = grid_for(c, units, k);
     // CRC-64 static split with fewer units than one full workgroup per CU:
     // one workgroup per unit, at most one per CU (each pays a 66 KiB LDS
     // fill); the kernel then numbers waves across workgroups first
-    if (width == 64 && !dyn_policy(width, aligned ? kFixedAligned : kFixedGeneric, nt, false) &&
-        units < (uint64_t)c->cus * (uint64_t)(k.block / 64))
+    if (width == 64 && !dyn && units < (uint64_t)c->cus * (uint64_t)(k.block / 64))
         blocks = (unsigned)(units < (uint64_t)c->cus ? (units ? units : 1) : c->cus);
+    SlotRef sr;
+    if (dyn) {
+        sr = queue_slot(c, stream);
+        a.queue = sr.q;
+    } else if (MCK_BAL && (width == 32 || MCK_BAL64) && aligned && !light && blocks >= kBalGroups && blocks <= kBalMaxWg &&
+               units >= (uint64_t)blocks * (uint64_t)(k.block / 64)) {
+        // the balanced static split (crc_gpu_device.h): a full grid only
+        sr = queue_slot(c, stream, true);
+        a.queue = sr.q;
+        a.bal = static_cast<BalBank *>(sr.bal);
+        a.bal_seq = sr.seq;
+    }
     int rc = launch(k, a, blocks, stream);
+    if (rc != MCHECKSUM_GPU_OK) slot_unissue(c, sr);
     if (rc == MCHECKSUM_GPU_OK && gpu_msb(idx)) rc = swap_outputs(dev_out, count, width, stream);
     return rc;
 }
@@ -560,7 +678,24 @@ long long mchecksum_gpu_queue_faults(void) {
     if (hipDeviceSynchronize() != hipSuccess) return -1;
     if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_mck_queue_faults), sizeof(n), 0, hipMemcpyDeviceToHost) != hipSuccess)
         return -1;
-    return n;
+    // mchecksum_gpu_ext.hip's kernels (the segment chunk queue) count into
+    // their own translation unit's copy of the counter
+    const long long ext = ext_queue_faults();
+    if (ext < 0) return -1;
+    return (long long)n + ext;
+}
+
+int mchecksum_gpu_queue_stats(long long *stats, size_t n) {
+    if (!stats) return set_err(MCHECKSUM_GPU_EINVAL, "NULL pointer argument");
+    if (!mchecksum_gpu_available()) return set_err(MCHECKSUM_GPU_ENODEV, "no HIP device");
+    std::lock_guard<std::mutex> lk(g_mu);
+    DevCtx *c = nullptr;
+    int rc = device_ctx(&c);
+    if (rc) return rc;
+    const long long v[MCHECKSUM_GPU_QSTAT_COUNT] = {c->n_slot, c->n_noslot, c->n_reclaim, c->n_busy_skip,
+                                                    (long long)c->sid_slot.size()};
+    for (size_t i = 0; i < n && i < MCHECKSUM_GPU_QSTAT_COUNT; i++) stats[i] = v[i];
+    return MCHECKSUM_GPU_OK;
 }
 
 #if MCK_TRACE
@@ -578,6 +713,21 @@ MCHECKSUM_PUBLIC int mck_debug_qwave_read(void *host, size_t bytes) {
 MCHECKSUM_PUBLIC int mck_debug_units_read(void *host, size_t bytes) {
     if (bytes > sizeof(g_mck_unit_end)) bytes = sizeof(g_mck_unit_end);
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_mck_unit_end), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+// ... the XCD of each wave of the last launch ...
+MCHECKSUM_PUBLIC int mck_debug_trace_xcc_read(void *host, size_t bytes) {
+    if (bytes > sizeof(g_mck_trace_xcc)) bytes = sizeof(g_mck_trace_xcc);
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_mck_trace_xcc), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+// ... the balanced split's two banks of slot `slot` on the current device ...
+MCHECKSUM_PUBLIC int mck_debug_bal_read(int slot, void *host, size_t bytes) {
+    DevCtx *c = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        if (device_ctx(&c) || slot < 0 || slot >= (int)kQueueSlots) return -1;
+    }
+    if (bytes > 2 * sizeof(BalBank)) bytes = 2 * sizeof(BalBank);
+    return hipMemcpy(host, static_cast<BalBank *>(c->bal) + 2 * (size_t)slot, bytes, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
 // ... and the work-queue fault records (count, then 4 words per record).
 MCHECKSUM_PUBLIC int mck_debug_qdiag_read(unsigned int *n, unsigned long long *rec) {

@@ -546,7 +546,18 @@ __global__ __launch_bounds__(256) void core_header_kernel(HdrArgs a) {
 // lane ranges hashed byte by byte, each shifted past the bytes after it
 // (Z^k from the base-16 digit tables) and XOR-reduced over the wave, then
 // L <- Z^n(L) ^ that.  CRC = L ^ Z^N(init) ^ xorout, N = hashed byte count.
+//
+// Large batches (the throughput layout, round 3) run the same walk in
+// persistent 1024-thread workgroups that also hold the payload kernels' LDS
+// tables: an opaque or raw field of >= kXdrFastMin bytes is hashed by the
+// payload step loop (coalesced 1 KiB steps, payload32_g64 / payload64_g64 in
+// RAW form: zero init, no finalisation) instead of 64 byte-serial lane
+// ranges, and messages come from the work queue (crc_gpu_device.h) -- an
+// iovec message (hg_perf_proc_iovec, Testing/perf/hg/mercury_perf.c:897-923:
+// a u32 length, then the bytes) then costs about what the same payload costs
+// through the offsets kernel.
 constexpr uint32_t kXdrMaxFields = 64;
+constexpr uint64_t kXdrFastMin = 256;
 
 struct XdrArgs {
     const uint8_t *buf;
@@ -555,6 +566,9 @@ struct XdrArgs {
     void *out;
     uint8_t *status;
     const void *shift;
+    const void *pack;                // throughput kernel: the model's G = 64 table pack
+    unsigned long long *queue;       // throughput kernel: work-queue slot (nullptr: static split)
+    uint32_t *err_word;              // throughput kernel: fail-closed report
     uint64_t rpoly, init, xorout;
     uint32_t nf;
     uint32_t kind[kXdrMaxFields], size[kXdrMaxFields];
@@ -569,66 +583,125 @@ __device__ __forceinline__ xdr_reg_t<W> xdr_shift(const void *sp, xdr_reg_t<W> x
     else return shift64(reinterpret_cast<const crc64_shift_pack_t *>(sp), x, n);
 }
 
+// Byte table of the register form (Z^1 of the low byte) for entry t < 256.
 template <int W>
-__global__ __launch_bounds__(256) void xdr_kernel(XdrArgs a) {
+__device__ __forceinline__ xdr_reg_t<W> xdr_tab_entry(uint64_t rpoly, uint32_t t) {
     using R = xdr_reg_t<W>;
-    __shared__ R tab[256];
-    {
-        R r = (R)threadIdx.x;  // byte table of the register form: Z^1 of the low byte
-        for (int k = 0; k < 8; k++) r = (r & 1u) ? (r >> 1) ^ (R)a.rpoly : r >> 1;
-        tab[threadIdx.x] = r;
-    }
-    __syncthreads();
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t nw = (uint64_t)gridDim.x * 4;
-    for (uint64_t m = uniform((uint32_t)(blockIdx.x * 4 + (threadIdx.x >> 6))); m < a.count; m += nw) {
-        uint64_t pos = a.off[m];
-        const uint64_t end = a.off[m + 1];
-        R acc = 0;
-        uint64_t N = 0, last = 0;
-        bool bad = end < pos;
-        for (uint32_t f = 0; f < a.nf && !bad; f++) {
-            const uint32_t kind = a.kind[f], sz = a.size[f];
-            if (kind == MCHECKSUM_XDR_SKIP_IF_ZERO) {
-                if (last == 0) f += sz;
-                continue;
-            }
-            if (kind == MCHECKSUM_XDR_INT) {
-                const uint32_t slot = sz <= 4 ? 4u : 8u;
-                if (end - pos < slot) {
-                    bad = true;
-                    break;
-                }
-                uint64_t v = 0;
-                for (uint32_t b = 0; b < slot; b++) v = v << 8 | a.buf[pos + b];
-                for (uint32_t b = 0; b < sz; b++) acc = (acc >> 8) ^ tab[(uint32_t)(acc ^ (R)(v >> (8 * b))) & 0xFFu];
-                last = sz == 8 ? v : v & ((1ull << (8 * sz)) - 1);
-                N += sz;
-                pos += slot;
-                continue;
-            }
-            const bool raw = kind == MCHECKSUM_XDR_RAW || kind == MCHECKSUM_XDR_RAW_LEN;
-            const uint64_t len = (kind == MCHECKSUM_XDR_OPAQUE_LEN || kind == MCHECKSUM_XDR_RAW_LEN) ? last : sz;
-            if (len > end - pos || (!raw && ((len + 3) & ~3ull) > end - pos)) {
+    R r = (R)t;
+    for (int k = 0; k < 8; k++) r = (r & 1u) ? (r >> 1) ^ (R)rpoly : r >> 1;
+    return r;
+}
+
+// One message (one wave, wave-uniform walk): writes out[m] and status[m].
+// fast(p, len, &L) may hash an opaque/raw field of len bytes at p itself
+// (returning true with L = its linear CRC); otherwise 64 lane ranges are
+// hashed byte by byte.
+template <int W, class Fast>
+__device__ __forceinline__ void xdr_message(const XdrArgs &a, uint64_t m, const xdr_reg_t<W> *tab, uint32_t lane,
+                                            Fast &&fast) {
+    using R = xdr_reg_t<W>;
+    uint64_t pos = a.off[m];
+    const uint64_t end = a.off[m + 1];
+    R acc = 0;
+    uint64_t N = 0, last = 0;
+    bool bad = end < pos;
+    for (uint32_t f = 0; f < a.nf && !bad; f++) {
+        const uint32_t kind = a.kind[f], sz = a.size[f];
+        if (kind == MCHECKSUM_XDR_SKIP_IF_ZERO) {
+            if (last == 0) f += sz;
+            continue;
+        }
+        if (kind == MCHECKSUM_XDR_INT) {
+            const uint32_t slot = sz <= 4 ? 4u : 8u;
+            if (end - pos < slot) {
                 bad = true;
                 break;
             }
+            uint64_t v = 0;
+            for (uint32_t b = 0; b < slot; b++) v = v << 8 | a.buf[pos + b];
+            for (uint32_t b = 0; b < sz; b++) acc = (acc >> 8) ^ tab[(uint32_t)(acc ^ (R)(v >> (8 * b))) & 0xFFu];
+            last = sz == 8 ? v : v & ((1ull << (8 * sz)) - 1);
+            N += sz;
+            pos += slot;
+            continue;
+        }
+        const bool raw = kind == MCHECKSUM_XDR_RAW || kind == MCHECKSUM_XDR_RAW_LEN;
+        const uint64_t len = (kind == MCHECKSUM_XDR_OPAQUE_LEN || kind == MCHECKSUM_XDR_RAW_LEN) ? last : sz;
+        if (len > end - pos || (!raw && ((len + 3) & ~3ull) > end - pos)) {
+            bad = true;
+            break;
+        }
+        R p = 0;
+        if (!fast(a.buf + pos, len, &p)) {
             const uint64_t chunk = (len + 63) / 64;
             const uint64_t lo = lane * chunk < len ? lane * chunk : len, hi = lo + chunk < len ? lo + chunk : len;
-            R p = 0;
             for (uint64_t i = lo; i < hi; i++) p = (p >> 8) ^ tab[(uint32_t)(p ^ a.buf[pos + i]) & 0xFFu];
             p = xdr_shift<W>(a.shift, p, len - hi);
 #pragma unroll
             for (int k = 1; k < 64; k <<= 1) p ^= __shfl_xor(p, k, 64);
-            acc = xdr_shift<W>(a.shift, acc, len) ^ p;
-            N += len;
-            pos += raw ? len : (len + 3) & ~3ull;
         }
-        if (lane == 0) {
-            const R crc = bad ? (R)0 : acc ^ xdr_shift<W>(a.shift, (R)a.init, N) ^ (R)a.xorout;
-            reinterpret_cast<R *>(a.out)[m] = crc;
-            if (a.status) a.status[m] = bad ? 1 : 0;
-        }
+        acc = xdr_shift<W>(a.shift, acc, len) ^ p;
+        N += len;
+        pos += raw ? len : (len + 3) & ~3ull;
+    }
+    if (lane == 0) {
+        const R crc = bad ? (R)0 : acc ^ xdr_shift<W>(a.shift, (R)a.init, N) ^ (R)a.xorout;
+        reinterpret_cast<R *>(a.out)[m] = crc;
+        if (a.status) a.status[m] = bad ? 1 : 0;
+    }
+}
+
+// Latency layout (small batches): 256-thread workgroups, a byte table only.
+template <int W>
+__global__ __launch_bounds__(256) void xdr_kernel(XdrArgs a) {
+    using R = xdr_reg_t<W>;
+    __shared__ R tab[256];
+    tab[threadIdx.x] = xdr_tab_entry<W>(a.rpoly, threadIdx.x);
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t nw = (uint64_t)gridDim.x * 4;
+    for (uint64_t m = uniform((uint32_t)(blockIdx.x * 4 + (threadIdx.x >> 6))); m < a.count; m += nw)
+        xdr_message<W>(a, m, tab, lane, [](const uint8_t *, uint64_t, R *) { return false; });
+}
+
+// Throughput layout (large batches): persistent 1024-thread workgroups with the
+// payload step loop's LDS tables (CRC-32C: the replicated byte tables, one
+// workgroup per CU; CRC-64: the 12-lookup tables with combine operators in
+// global memory) and the byte table after them; messages from the work queue.
+template <int W>
+constexpr uint32_t kXdrMainLds = W == 32 ? kL32Bytes : kL64Main;
+
+template <int W, bool NT>
+__global__ __launch_bounds__(1024, 1) void xdr_fast_kernel(XdrArgs a) {
+    using R = xdr_reg_t<W>;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kXdrMainLds<W> + 256 * sizeof(R)];
+    __shared__ WgQueue wgq;
+    R *tab = reinterpret_cast<R *>(lds + kXdrMainLds<W>);
+    if (threadIdx.x == 0) wg_queue_init(&wgq, a.queue, a.count);
+    if constexpr (W == 32) fill_lds32<false, 1024>(lds, reinterpret_cast<const crc32_gpu_pack_t *>(a.pack));
+    else fill_lds64<1024, kOpsGlobal>(lds, reinterpret_cast<const crc64_gpu_pack_t *>(a.pack));
+    if (threadIdx.x < 256) tab[threadIdx.x] = xdr_tab_entry<W>(a.rpoly, threadIdx.x);
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 16u + (threadIdx.x >> 6));
+    const uint32_t nw = gridDim.x * 16u;
+    const uint32_t lc0 = (lane & 31u) << 2, lc1 = lc0 | 0x10000u, lc64 = (lane & 31u) << 3;
+    auto fast = [&](const uint8_t *p, uint64_t len, R *out) -> bool {
+        if (len < kXdrFastMin || len >= (1ull << 31)) return false;
+        if constexpr (W == 32)
+            *out = payload32_g64<NT, Tab32<false>, true>(Tab32<false>{lds}, reinterpret_cast<const crc32_gpu_pack_t *>(a.pack),
+                                                         p, len, lane, lc0, lc1);
+        else
+            *out = payload64_g64<NT, true, kOpsGlobal>(lds, reinterpret_cast<const crc64_gpu_pack_t *>(a.pack), p, len,
+                                                       lane, lc64);
+        return true;
+    };
+    const bool faulted = for_each_unit<true>(&wgq, a.queue, a.count, wave, nw,
+                                             [&](uint64_t m) { xdr_message<W>(a, m, tab, lane, fast); });
+    if (faulted) {  // fail closed: the caller's error word, and every status flagged
+        if (lane == 0 && a.err_word) atomicAdd(a.err_word, 1u);
+        if (a.status)
+            for (uint64_t m = lane; m < a.count; m += 64) a.status[m] = 1;
     }
 }
 
@@ -691,6 +764,13 @@ int get_ext(DevCtx *c, int idx, const void **out) {
     c->ext[idx] = d;
     *out = d;
     return 0;
+}
+
+long long ext_queue_faults() {
+    unsigned int n = 0;
+    if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_mck_queue_faults), sizeof(n), 0, hipMemcpyDeviceToHost) != hipSuccess)
+        return -1;
+    return n;
 }
 
 }  // namespace mck
@@ -758,7 +838,6 @@ int mchecksum_gpu_checksum_segments(const char *hash_method, const uint64_t *dev
     a.pack = pack;
     a.shift = shift;
     a.err_word = error_word();
-    if (MCK_SEG_QUEUE && width == 64) a.queue = queue_slot(c, stream);
     const uint64_t out_words = (uint64_t)nobj * (uint64_t)(width / 32);
     // at least one block per scan block, and enough to zero the output quickly
     uint64_t zgrid = (out_words + kScanThreads - 1) / kScanThreads;
@@ -787,9 +866,17 @@ int mchecksum_gpu_checksum_segments(const char *hash_method, const uint64_t *dev
     if (width == 32) {
         hipLaunchKernelGGL((seg_kernel<32, 0>), dim3(c->cus), dim3(1024), 0, s, a);
     } else {
+        // the aligned chunk pass takes the work queue; the ragged pass never
+        // touches the slot (a.queue is cleared for it)
+        const SlotRef sr = MCK_SEG_QUEUE ? queue_slot(c, stream) : SlotRef{};
+        a.queue = sr.q;
         hipLaunchKernelGGL((seg_kernel<64, 1>), dim3(2 * c->cus), dim3(1024), 0, s, a);
         e = hipGetLastError();
-        if (e != hipSuccess) return hip_err(e, "segment kernel launch");
+        if (e != hipSuccess) {
+            slot_unissue(c, sr);
+            return hip_err(e, "segment kernel launch");
+        }
+        a.queue = nullptr;
         hipLaunchKernelGGL((seg_kernel<64, 2>), dim3(c->cus), dim3(1024), 0, s, a);
     }
     e = hipGetLastError();
@@ -874,6 +961,17 @@ int mchecksum_gpu_checksum_xdr(const char *hash_method, const mchecksum_xdr_fiel
         if (rc) return rc;
     }
     if (count == 0) return MCHECKSUM_GPU_OK;
+    // throughput layout for batches past a receive queue's worth of RPCs
+    // (MCHECKSUM_GPU_XDR_FAST=0/1 overrides)
+    const char *fenv = getenv("MCHECKSUM_GPU_XDR_FAST");
+    const bool fast = fenv && fenv[0] ? fenv[0] == '1' : count > 1024;
+    if (fast) {
+        int w2 = 0;
+        const void *pack = nullptr;
+        int rc = prologue(hash_method, CRC_GPU_MAX_LOG2G, &w2, &c, &pack);
+        if (rc) return rc;
+        a.pack = pack;
+    }
     const mck_model_t &m = mck_models[idx];
     a.buf = (const uint8_t *)dev_buf;
     a.off = dev_msg_offsets;
@@ -885,6 +983,26 @@ int mchecksum_gpu_checksum_xdr(const char *hash_method, const mchecksum_xdr_fiel
     a.init = mck_reflect(m.init, m.width);
     a.xorout = m.xorout;
     a.nf = (uint32_t)nfields;
+    if (fast) {
+        // non-temporal loads for batches far past the Infinity Cache, sized
+        // by count as for offsets batches (MCHECKSUM_GPU_NT=0/1 overrides)
+        const char *nenv = getenv("MCHECKSUM_GPU_NT");
+        const bool nt = nenv && nenv[0] ? nenv[0] == '1' : count >= 8192;
+        a.err_word = error_word();
+        const SlotRef sr = queue_slot(c, stream);
+        a.queue = sr.q;
+        uint64_t blocks = (count + 15) / 16;
+        if (blocks > (uint64_t)c->cus) blocks = (uint64_t)c->cus;
+        auto k = width == 32 ? (nt ? xdr_fast_kernel<32, true> : xdr_fast_kernel<32, false>)
+                             : (nt ? xdr_fast_kernel<64, true> : xdr_fast_kernel<64, false>);
+        hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(1024), 0, (hipStream_t)stream, a);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) {
+            slot_unissue(c, sr);
+            return hip_err(e, "XDR kernel launch");
+        }
+        return MCHECKSUM_GPU_OK;
+    }
     uint64_t blocks = (count + 3) / 4;
     if (blocks > (uint64_t)c->cus * 8) blocks = (uint64_t)c->cus * 8;
     if (width == 32) hipLaunchKernelGGL(xdr_kernel<32>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);

@@ -79,6 +79,21 @@ def queue_faults() -> int:
     return int(_lib().mchecksum_gpu_queue_faults())
 
 
+QSTAT_KEYS = ("slot", "noslot", "reclaim", "busy_skip", "owners")
+
+
+def queue_stats() -> dict:
+    """Work-queue slot bookkeeping of the current device (mchecksum_gpu_queue_stats):
+    launches given a slot, launches without one, slot owner changes, busy slots
+    passed over, streams owning a slot."""
+    import ctypes
+    buf = (ctypes.c_longlong * len(QSTAT_KEYS))()
+    rc = _lib().mchecksum_gpu_queue_stats(buf, len(QSTAT_KEYS))
+    if rc:
+        _err(rc, "queue_stats")
+    return dict(zip(QSTAT_KEYS, (int(v) for v in buf)))
+
+
 def set_error_word(word: torch.Tensor | None) -> None:
     """Fail-closed report (mchecksum_gpu_set_error_word): every later batch call
     of this host thread adds 1 to `word` (a one-element device int32 tensor the
@@ -320,7 +335,7 @@ XDR_INT, XDR_OPAQUE, XDR_OPAQUE_LEN, XDR_RAW, XDR_RAW_LEN, XDR_SKIP_IF_ZERO = 0,
 
 
 def checksum_xdr(method: str, data: torch.Tensor, msg_offsets: torch.Tensor, schema, status: bool = False,
-                 stream=None, offsets_host=None):
+                 stream=None, offsets_host=None, out: torch.Tensor | None = None):
     """Proc checksum of messages serialized in XDR mode (include/mchecksum_gpu.h,
     mchecksum_gpu_checksum_xdr): schema = [(kind, size), ...] with the XDR_*
     kinds.  Returns the CRC tensor, or (CRCs, status) with status=True
@@ -331,7 +346,10 @@ def checksum_xdr(method: str, data: torch.Tensor, msg_offsets: torch.Tensor, sch
     _same_device(data, msg_offsets=msg_offsets)
     count = msg_offsets.numel() - 1
     fields = (XdrField * max(1, len(schema)))(*[XdrField(int(k), int(z)) for k, z in schema])
-    out = torch.empty(max(count, 0), dtype=out_dtype(method), device=data.device)
+    if out is None:
+        out = torch.empty(max(count, 0), dtype=out_dtype(method), device=data.device)
+    elif out.numel() < count or out.dtype != out_dtype(method) or out.device != data.device:
+        raise GpuChecksumError("out tensor has the wrong size, dtype or device")
     st = torch.ones(max(count, 0), dtype=torch.uint8, device=data.device) if status else None
     with _on(data):
         rc = _lib().mchecksum_gpu_checksum_xdr(method.encode(), fields, len(schema), data.data_ptr(),

@@ -1,0 +1,126 @@
+"""bench.py's N > 1 JSON line on the CPU: 2 gloo ranks each checksum their
+share of one global batch (the oracle standing in for the GPU kernels on a
+CPU-only box), gather it with bench.gather_shares, and rank 0 builds the line
+with bench.report -- the same code the GPU run executes after timing.  The line
+must carry the CPU baseline (timed on rank 0's host at N > 1 too), a parity
+verdict from the ORACLE over every share, and a labelled roofline.traffic."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+LAYOUTS = {
+    # name: (bench config, method, global count, payload length, seed, layout)
+    "fixed": ("c5", "crc32c", 96, 65536, 0x4D43310000000005, "fixed"),
+    "offsets": ("c4", "crc32c", 300, None, 0x4D43310000000004, "offsets"),
+    "messages": ("msgs", "crc32c", 300, None, 0x4D43310000000004, "messages"),
+    "segments": ("seg", "crc64", 6, 1 << 20, 0x4D43310000000003, "segments"),
+}
+
+
+def _share_crcs(O, bench, name, rank, world):
+    """(local CRC array, plan, rank-local offsets) of this rank's share."""
+    from mercury_amd.shard import batch_shard
+    from mercury_amd.workload import segment_slots, varlen_offsets
+    cfg, method, gc, length, seed, layout = LAYOUTS[name]
+    if layout == "fixed":
+        plan = batch_shard(rank, world, gc, length)
+        local = O.splitmix_bytes(plan.nbytes, seed, first_word=plan.first_word)
+        return O.batch_fixed(method, local, length, length, plan.count), plan, None
+    if layout == "segments":  # weak: gc objects per rank from seed ^ rank
+        slots = segment_slots(seed ^ rank, gc * bench.SEGS_PER_OBJECT)
+        crcs = [O.crc(method, bench._segment_object_bytes(O, seed ^ rank, length, j, slots)) for j in range(gc)]
+        return np.array(crcs, dtype=np.uint64), None, None
+    plan = batch_shard(rank, world, gc, offsets_global=varlen_offsets(seed, gc))
+    local = O.splitmix_bytes(plan.nbytes, seed, first_word=plan.first_word)
+    if layout == "offsets":
+        return O.batch_offsets(method, local, plan.offsets), plan, plan.offsets
+    inter = np.empty(2 * plan.count + 1, dtype=np.uint64)  # sender pieces: header, payload
+    inter[0::2] = plan.offsets
+    inter[1::2] = plan.offsets[:-1] + np.uint64(20)
+    return O.batch_offsets(method, local, inter), plan, plan.offsets
+
+
+def _worker(name, corrupt, rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    from types import SimpleNamespace
+
+    import torch
+    import torch.distributed as dist
+
+    import bench
+    from oracle import oracle as O
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfg, method, gc, length, seed, layout = LAYOUTS[name]
+    crcs, plan, off = _share_crcs(O, bench, name, rank, world)
+    if corrupt and rank == 1:
+        crcs = crcs.copy()
+        crcs[1 if layout == "messages" else 0] ^= np.uint64(1)  # the first payload of rank 1's share
+    dt = np.int32 if method == "crc32c" else np.int64
+    t = torch.from_numpy(crcs.astype(np.uint32 if method == "crc32c" else np.uint64).view(dt).copy())
+    count = plan.count if plan is not None else gc
+    counts = plan.counts if plan is not None else [gc] * world
+    if layout == "messages":
+        counts = [2 * c for c in counts]
+    full = bench.gather_shares(dist, t, counts, world, torch.device("cpu"))
+    if rank == 0:
+        got = full.numpy().view(np.uint32 if method == "crc32c" else np.uint64)
+        args = SimpleNamespace(steps=3, warmup=1, cpu_seconds=0.05, parity_samples=16, no_cpu_baseline=False)
+        payload_bytes = count * length if length else int(off[-1] - off[0])
+        r = SimpleNamespace(
+            config=cfg, method=method, seed=seed, length=length, layout=layout, strong=layout != "segments",
+            global_count=gc if layout != "segments" else gc * world, count=count, plan=plan,
+            payload_bytes=payload_bytes, alg_bytes=payload_bytes + 4 * count, gib_s=1.0, wall_max=0.003,
+            kern_ms_max=1.0, achieved=1.0, per_rank=[[0.003, 1.0]] * world, world=world, got=got, offsets_host=off,
+            verify_note=None, lanes=64)
+        q.put(bench.report(args, r))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _run(name, corrupt=False):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(name, corrupt, r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(300)
+        assert p.exitcode == 0
+    return q.get()
+
+
+@pytest.mark.parametrize("name", sorted(LAYOUTS))
+def test_two_rank_line_has_baseline_oracle_parity_and_traffic(name):
+    res = _run(name)
+    cb = res["cpu_baseline"]
+    assert cb["kind"] == "port" and cb["unit"] == "GiB/s" and cb["value"] > 0 and cb["cores"] >= 1
+    assert cb["sample"] and "breakdown_GiB_s" in cb
+    assert res["parity"].startswith("bit-exact (") and "across all 2 shares vs oracle" in res["parity"], res["parity"]
+    assert res["n_gpus"] == 2 and res["world_size"] == 2 and len(res["per_rank"]) == 2
+    roof = res["roofline"]
+    assert roof["traffic"] is not None and "rank 0's share" in roof["traffic_source"], roof
+    assert res["scaling"] == ("weak" if name == "segments" else "strong")
+
+
+@pytest.mark.parametrize("name", ["fixed", "messages"])
+def test_two_rank_line_flags_a_wrong_share(name):
+    """A wrong CRC in rank 1's share reads as a mismatch, not as bit-exact."""
+    res = _run(name, corrupt=True)
+    assert res["parity"].startswith("MISMATCH 1/") and "across all 2 shares" in res["parity"], res["parity"]

@@ -39,6 +39,10 @@ def qlib(gpu):
                                                c.c_void_p, c.c_void_p]
     L.mchecksum_gpu_verify_offsets.argtypes = [c.c_char_p, c.c_void_p, c.c_void_p, c.c_size_t, c.c_void_p,
                                                c.c_void_p, c.c_void_p, c.c_void_p]
+    L.mchecksum_gpu_checksum_segments.argtypes = [c.c_char_p, c.c_void_p, c.c_void_p, c.c_size_t, c.c_void_p,
+                                                  c.c_size_t, c.c_void_p, c.c_size_t, c.c_void_p, c.c_void_p]
+    L.mchecksum_gpu_segments_work_size.argtypes = [c.c_size_t]
+    L.mchecksum_gpu_segments_work_size.restype = c.c_size_t
     L.mchecksum_gpu_set_error_word.argtypes = [c.c_void_p]
     L.mchecksum_gpu_queue_faults.restype = c.c_longlong
     return L
@@ -126,6 +130,43 @@ def test_large_fixed_batch_fault(gpu, qlib):
     torch.cuda.synchronize()
     assert int(word.item()) == 1
     assert int((out != want).sum().item()) == 1
+
+
+def test_segment_chunk_queue_fault(gpu, qlib):
+    """The CRC-64 scatter-gather chunk pass (mchecksum_gpu_ext.hip, seg_kernel
+    with the work queue) in the fault-injecting build: the dropped chunk leaves
+    exactly one object wrong, the caller's error word gets +1, and the
+    process-wide fault count (which sums both translation units' counters)
+    rises by one."""
+    import torch
+    nobj, nseg_per, seg = 128, 4, 1 << 20  # 2048 aligned 256 KiB chunks: two+ per workgroup
+    data = torch.empty(nobj * nseg_per * seg + 64, dtype=torch.uint8, device="cuda")
+    gpu.fill_splitmix(data, 0x5E6F)
+    segs = [data[i * seg:(i + 1) * seg] for i in range(nobj * nseg_per)]
+    first = np.arange(0, nobj * nseg_per + 1, nseg_per)
+    batch = gpu.SegmentBatch(segs, first)
+    want = batch.checksum("crc64").clone()
+    torch.cuda.synchronize()
+    out = ~want
+    word = torch.zeros(1, dtype=torch.int32, device="cuda")
+    n = batch.nseg
+    base = batch.meta.data_ptr()
+    faults0 = qlib.mchecksum_gpu_queue_faults()
+    assert qlib.mchecksum_gpu_prepare(b"crc64") == 0
+    work = torch.empty((qlib.mchecksum_gpu_segments_work_size(n) + 7) // 8, dtype=torch.int64, device="cuda")
+    qlib.mchecksum_gpu_set_error_word(word.data_ptr())
+    try:
+        rc = qlib.mchecksum_gpu_checksum_segments(b"crc64", base, base + 8 * n, n, base + 16 * n, batch.nobj,
+                                                  work.data_ptr(), work.numel() * 8, out.data_ptr(),
+                                                  torch.cuda.current_stream().cuda_stream)
+    finally:
+        qlib.mchecksum_gpu_set_error_word(None)
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert int(word.item()) == 1, "a chunk pass that dropped a chunk must bump the error word"
+    assert qlib.mchecksum_gpu_queue_faults() - faults0 == 1, "the segment kernels' fault count must be reported"
+    lost = np.nonzero((out != want).cpu().numpy())[0]
+    assert len(lost) == 1, lost[:8]
 
 
 def test_product_library_reports_no_fault(gpu, batch):

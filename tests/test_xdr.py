@@ -88,9 +88,16 @@ def _run(gpu, method, msgs, schema, status=False):
     return gpu.as_unsigned(r)
 
 
+# both kernel layouts: "0" the latency layout (byte-table walk), "1" the
+# throughput layout (payload step loop for fields >= 256 B, work queue)
+LAYOUTS = ["0", "1"]
+
+
 @pytest.mark.gpu
+@pytest.mark.parametrize("layout", LAYOUTS)
 @pytest.mark.parametrize("method", ["crc32c", "crc64"])
-def test_gpu_xdr_test_proc_fixtures(gpu, method):
+def test_gpu_xdr_test_proc_fixtures(gpu, method, layout, monkeypatch):
+    monkeypatch.setenv("MCHECKSUM_GPU_XDR_FAST", layout)
     for name, e in GOLD["payloads"].items():
         schema = [tuple(f) for f in e["xdr_schema"]]
         got = _run(gpu, method, [bytes.fromhex(e["xdr_hex"])] * 3, schema)
@@ -98,9 +105,11 @@ def test_gpu_xdr_test_proc_fixtures(gpu, method):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("layout", LAYOUTS)
 @pytest.mark.parametrize("method", ["crc32c", "crc64"])
 @pytest.mark.parametrize("kind", ["iovec", "mixed"])
-def test_gpu_xdr_random_messages(gpu, oracle_mod, method, kind):
+def test_gpu_xdr_random_messages(gpu, oracle_mod, method, kind, layout, monkeypatch):
+    monkeypatch.setenv("MCHECKSUM_GPU_XDR_FAST", layout)
     O = oracle_mod
     schema = _schemas(O)[kind]
     rng = np.random.default_rng(17 if kind == "iovec" else 18)
@@ -112,7 +121,9 @@ def test_gpu_xdr_random_messages(gpu, oracle_mod, method, kind):
 
 
 @pytest.mark.gpu
-def test_gpu_xdr_truncated_messages_are_flagged(gpu, oracle_mod):
+@pytest.mark.parametrize("layout", LAYOUTS)
+def test_gpu_xdr_truncated_messages_are_flagged(gpu, oracle_mod, layout, monkeypatch):
+    monkeypatch.setenv("MCHECKSUM_GPU_XDR_FAST", layout)
     O = oracle_mod
     schema = _schemas(O)["mixed"]
     rng = np.random.default_rng(5)
@@ -124,6 +135,25 @@ def test_gpu_xdr_truncated_messages_are_flagged(gpu, oracle_mod):
     for i, m in enumerate(msgs):
         if i not in cut:
             assert int(got[i]) == O.crc("crc32c", O.xdr_hashed_stream(schema, m))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("method", ["crc32c", "crc64"])
+def test_gpu_xdr_large_iovec_batch(gpu, oracle_mod, method):
+    """A batch past 1024 messages takes the throughput layout by default:
+    5000 hg_perf_proc_iovec messages of C4's length mix (u32 length, bytes,
+    zero pad), every CRC equal to the oracle's over the hashed stream (the
+    host-order length, then the bytes)."""
+    import torch
+    from mercury_amd.workload import varlen_lengths
+    O = oracle_mod
+    schema = _schemas(O)["iovec"]
+    lens = varlen_lengths(0x4D43310000000004, 5000).astype(np.int64)
+    rng = np.random.default_rng(23)
+    msgs = [O.xdr_encode(schema, [int(n), rng.integers(0, 256, int(n), dtype=np.uint8).tobytes()]) for n in lens]
+    got = _run(gpu, method, msgs, schema)
+    want = [O.crc(method, O.xdr_hashed_stream(schema, m)) for m in msgs]
+    assert got.tolist() == want
 
 
 @pytest.mark.gpu

@@ -1,0 +1,66 @@
+#!/bin/bash
+# Round-3 GPU passes.  PART selects one:
+#   tests  -- new slot / fail-closed tests first, then the whole -m gpu suite
+#   ab     -- in-process A/B: working tree (cur) vs last commit (prev) and the
+#             balanced split switched off (BALOFF) on AB_CONFIGS
+#   bench  -- bench.py per CONFIGS into gpurun_out/r03/bench_<config>.json
+#   trace  -- rocprofv3 kernel-trace summaries of bench.py per CONFIGS
+#   pmc    -- FETCH_SIZE / WRITE_SIZE passes per CONFIGS -> pmc_traffic_<config>.json
+# Every GPU step has its own time limit; the first failure ends the script.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-/root/repo}
+cd "$R"; mkdir -p gpurun_out/r03
+O="$R/gpurun_out/r03"
+step() { echo "== $1 $(date +%T)"; }
+for P in ${PART:-tests}; do
+if [ "$P" = tests ]; then
+  step "new tests"
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_slots.py tests/test_gpu_fail_closed.py -m gpu -x -v --timeout 300 \
+    --timeout-method thread > $O/pytest_new.log 2>&1; rc=$?
+  tail -15 $O/pytest_new.log
+  [ $rc -eq 0 ] || { grep -E "Error|assert|FAILED|^E " $O/pytest_new.log | head -60; exit $rc; }
+  step "full suite"
+  timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+    > $O/pytest_gpu.log 2>&1; rc=$?
+  tail -5 $O/pytest_gpu.log
+  [ $rc -eq 0 ] || { grep -E "Error|assert|FAILED|^E " $O/pytest_gpu.log | head -60; exit $rc; }
+fi
+if [ "$P" = ab ]; then
+  step "ab ${AB_CONFIGS:-c2,metric}"
+  timeout -k 10 600 python tools/ab_variants.py --config ${AB_CONFIGS:-c2,metric} --variants ${AB_VARIANTS:-prev cur} \
+    ${AB_ENV:---env BALOFF=MCHECKSUM_GPU_BAL=0} --rounds ${AB_ROUNDS:-6} --iters ${AB_ITERS:-10} \
+    --out $O/ab_${AB_TAG:-r03}.json > $O/ab_${AB_TAG:-r03}.log 2>&1; rc=$?
+  grep -v amdgpu.ids $O/ab_${AB_TAG:-r03}.log; [ $rc -eq 0 ] || exit $rc
+fi
+if [ "$P" = bench ]; then
+  for c in ${CONFIGS:-metric c2}; do
+    step "bench $c"
+    timeout -k 10 300 python bench.py --config $c ${BENCH_ARGS:-} > $O/bench_$c.json 2> $O/bench_$c.err || { tail -20 $O/bench_$c.err; exit 1; }
+    cat $O/bench_$c.json
+  done
+fi
+if [ "$P" = driver ]; then
+  step "bench driver-style"
+  timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_driver.json 2> $O/bench_driver.err || { tail -20 $O/bench_driver.err; exit 1; }
+  cat $O/bench_driver.json
+fi
+if [ "$P" = trace ]; then
+  cd /tmp && export TMPDIR=/tmp
+  for c in ${CONFIGS:-c2}; do
+    step "kernel trace $c"
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$c -o bench -- python3 $R/bench.py --config $c ${BENCH_ARGS:-} > $O/prof_bench_$c.json 2> $O/prof_bench_$c.err || { tail $O/prof_bench_$c.err; exit 1; }
+    cat $O/prof_bench_$c.json
+  done
+  cd "$R"
+fi
+if [ "$P" = pmc ]; then
+  cd /tmp && export TMPDIR=/tmp
+  for c in ${CONFIGS:-c4}; do
+    step "pmc $c"
+    timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/tr_${c}_f -o p -- python3 $R/tools/kernel_run.py --config $c --iters 4 > $O/tr_${c}_f.log 2>&1 || { tail $O/tr_${c}_f.log; exit 1; }
+    timeout -k 10 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/tr_${c}_w -o p -- python3 $R/tools/kernel_run.py --config $c --iters 4 > $O/tr_${c}_w.log 2>&1 || { tail $O/tr_${c}_w.log; exit 1; }
+    python3 $R/tools/pmc_traffic.py $O/tr_${c}_f $O/tr_${c}_w batch_kernel $O/pmc_traffic_$c.json $(python3 $R/tools/alg_bytes.py $c) 1 4 || exit 1
+  done
+  cd "$R"
+fi
+done
