@@ -27,9 +27,8 @@
  * Streams: `stream` is a hipStream_t (NULL = the default stream).  Calls are
  * asynchronous and capture-safe once mchecksum_gpu_prepare() has run for the
  * method on the current device (it uploads the lookup tables).  Large batches
- * balance their payloads through a device-side slot of their stream's own: a
- * work queue, or for mid-sized fixed batches a split re-weighted from the
- * previous launch's per-XCD times (launches on one stream never overlap).
+ * balance their payloads through a device-side work-queue slot of their
+ * stream's own (launches on one stream never overlap).
  * (A handle names a new stream only after hipStreamDestroy of the old one,
  * which returns once that stream's work has completed, so a reused handle
  * never shares its slot with launches in flight.)  A device has 2048 slots; once all are owned,
@@ -237,8 +236,8 @@ mchecksum_gpu_queue_faults(void);
 
 /* Diagnostics: work-queue slot bookkeeping of the current device since the
  * library was loaded, written to stats[0 .. min(n, MCHECKSUM_GPU_QSTAT_COUNT)):
- * launches given a slot, launches that took the plain static split without
- * one (graph captures, MCHECKSUM_GPU_BAL=0, no idle slot), slots that changed
+ * launches given a slot, launches that took the static split for want of one
+ * (graph captures, hipStreamPerThread, no idle slot), slots that changed
  * owner stream, busy slots passed over while looking for one, and streams
  * that currently own a slot.  Host-side counters only: no device sync. */
 #define MCHECKSUM_GPU_QSTAT_SLOT 0

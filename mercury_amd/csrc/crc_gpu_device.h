@@ -126,10 +126,19 @@ constexpr int kRingOff64 = kCrc64OffTwo ? 4 : kRingOff;
 // or the butterflies (ops 1..6) in LDS and the rest global
 enum OpsMode : int { kOpsLds = 0, kOpsGlobal = 1, kOpsMix = 2 };
 
+// A/B knobs for the aligned CRC-64 loop (round 3): one 1024-thread workgroup
+// per CU instead of two (128 VGPRs instead of 64: no spills, room for a deeper
+// load ring, MCK_RING64) -- half the waves to hide the LDS latency.
+#ifndef MCK_CRC64_ONE_WG
+#define MCK_CRC64_ONE_WG 0
+#endif
+#ifndef MCK_RING64
+#define MCK_RING64 MCK_RING
+#endif
 template <int W, int MODE, bool LIGHT = false>
 struct Shape {
     static constexpr bool ops_global = W == 64 && MODE == 0 && (MCK_CRC64_SPLIT || MCK_CRC64_P6);  // 0 = kFixedAligned
-    static constexpr bool two = W == 64 && (MODE == 0 || (MODE == 2 && kCrc64OffTwo));
+    static constexpr bool two = W == 64 && ((MODE == 0 && !MCK_CRC64_ONE_WG) || (MODE == 2 && kCrc64OffTwo));
     static constexpr int block = LIGHT ? kLightBlock : two ? MCK_BLOCK64 : kBlock;
     static constexpr int blocks_per_cu = LIGHT ? 8 : two ? 2 : 1;
     static constexpr int ops_mode = ops_global ? kOpsGlobal : (W == 64 && MODE == 2 && kCrc64OffMix) ? kOpsMix : kOpsLds;
@@ -170,10 +179,6 @@ struct BatchArgs {
     // MSB-first model on a verify call: the kernel's value is the CRC
     // byte-swapped (crc_gpu_layout.h), so swap before comparing
     uint32_t bswap;
-    // feedback-balanced static split (BalBank below): the slot's two banks
-    // and this launch's sequence number on them; nullptr = plain split
-    struct BalBank *bal;
-    uint32_t bal_seq;
 };
 // Piece size of a split payload: 256 KiB = 256 steps of the G = 64 loop.
 constexpr uint64_t kSplitBytes = 256u << 10;
@@ -408,56 +413,6 @@ __device__ __attribute__((unused)) void wg_queue_init(WgQueue *L, unsigned long 
     (void)wg_publish(L, 0, wg_fetch(L, q, plan.nch), plan.cl);
 }
 
-// ------------------------------------------------ balanced static split --
-// The plain static split (units wave, wave + #waves, ...) ends when the
-// slowest XCD ends: the per-XCD mean end of C2's waves spans 33.0-40.5 us
-// (profiles/r02/tail_trace_c2_static.json), and the work queue that would
-// balance it costs more per chunk fetch than it saves on a 44 us launch
-// (profiles/r02/ab_queue_chunks_c2.log).  Feedback instead: every launch on a
-// slot records, per workgroup, its entry stamp and the exit stamp of its last
-// wave; the next launch on the slot turns them into the time each group of
-// workgroups (blockIdx % 8, the XCD dispatch order) took for its share and
-// apportions its own units in proportion to the groups' measured rates (an
-// EMA over launches).  Nothing goes through the host and nothing waits
-// inside a launch.  Every workgroup computes the same shares from the same
-// record -- the previous launch on the slot has completed and launches on a
-// slot never overlap (queue_slot, mchecksum_gpu.hip) -- so the split is
-// exact: every unit exactly once, whatever the weights.  Two banks: launch s
-// reads bank s & 1 and writes bank (s + 1) & 1.
-//
-// Units go out in rounds of MCK_BAL_ROUND x #waves: round r gives group g
-// the units [base + c_g, base + c_(g+1)), c = the cumulative weights scaled
-// to the round, and the group's waves stride over them -- every XCD stays in
-// the same moving window of the batch, as with the plain split.
-#ifndef MCK_BAL
-#define MCK_BAL 1
-#endif
-#ifndef MCK_BAL64
-#define MCK_BAL64 0
-#endif
-#ifndef MCK_BAL_ROUND
-#define MCK_BAL_ROUND 1
-#endif
-#ifndef MCK_BAL_ALPHA
-#define MCK_BAL_ALPHA 0.5f
-#endif
-constexpr uint32_t kBalGroups = kQSub;
-constexpr uint32_t kBalMaxWg = 512;
-constexpr uint32_t kBalOne = 1u << 24;  // weights are fixed point, summing to kBalOne
-struct BalBank {
-    uint32_t grid;           // workgroups of the launch that wrote this bank (0: none yet)
-    uint32_t w[kBalGroups];  // the group weights that launch used
-    uint32_t pad[7];
-    unsigned long long rec[2 * kBalMaxWg];  // per workgroup: entry stamp, exit stamp of its last wave
-};
-struct BalLds {
-    uint32_t cut[kBalGroups + 1];  // cumulative weights of this launch
-    uint32_t span[kBalGroups];     // the previous launch's time per group (100 MHz ticks)
-    uint32_t hdr[1 + kBalGroups];  // the previous launch's grid and weights
-    uint32_t exited;
-    unsigned long long start;
-};
-
 template <typename T>
 __device__ __forceinline__ T wave_max(T v) {
 #pragma unroll
@@ -466,114 +421,6 @@ __device__ __forceinline__ T wave_max(T v) {
         v = o > v ? o : v;
     }
     return v;
-}
-template <typename T>
-__device__ __forceinline__ T wave_min(T v) {
-#pragma unroll
-    for (int k = 1; k < 64; k <<= 1) {
-        const T o = __shfl_xor(v, k, 64);
-        v = o < v ? o : v;
-    }
-    return v;
-}
-
-// What a lane loads of the previous launch's bank before the LDS fill, so the
-// loads' latency hides under the fill: wave g < 8 the records of workgroups
-// g, g + 8, ... (all 512 -- which of them the launch had is only known from
-// the header, so masking waits until after the fill); wave 8 the header.
-struct BalPre {
-    unsigned long long s, e;
-    uint32_t h;
-};
-
-__device__ __forceinline__ BalPre bal_prefetch(const BatchArgs &a, BalLds *bl) {
-    const uint32_t wib = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-    const BalBank *pb = a.bal + (a.bal_seq & 1u);
-    BalPre p{~0ull, 0ull, 0u};
-    if (threadIdx.x == 0) {
-        bl->start = wall_clock64();
-        bl->exited = 0;
-    }
-    if (wib < kBalGroups) {
-        const uint32_t j = wib + kBalGroups * lane;  // < kBalMaxWg
-        p.s = pb->rec[2 * j];
-        p.e = pb->rec[2 * j + 1];
-    } else if (wib == kBalGroups && lane <= kBalGroups) {
-        p.h = lane == 0 ? pb->grid : pb->w[lane - 1];
-    }
-    return p;
-}
-
-// After the fill, before its barrier: wave 8 stores the header; waves
-// g < 8 keep their records in registers for bal_span (after the barrier,
-// when the header's grid is known in LDS).
-__device__ __forceinline__ void bal_stash(BalLds *bl, const BalPre &p) {
-    const uint32_t wib = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-    if (wib == kBalGroups && lane <= kBalGroups) bl->hdr[lane] = p.h;
-}
-
-// After the fill barrier: wave g reduces group g's records (of workgroups the
-// previous launch had) to the group's time span; then thread 0 of every
-// workgroup turns spans and weights into this launch's cuts (identical inputs
-// -> identical cuts), workgroup 0 records the weights for the next launch.
-// Two barriers.
-__device__ __forceinline__ void bal_plan(const BatchArgs &a, BalLds *bl, const BalPre &p) {
-    const uint32_t wib = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-    const uint32_t grid = bl->hdr[0];
-    if (wib < kBalGroups) {
-        const bool live = grid <= kBalMaxWg && wib + kBalGroups * lane < grid;
-        const unsigned long long s = wave_min(live ? p.s : ~0ull), e = wave_max(live ? p.e : 0ull);
-        if (lane == 0) bl->span[wib] = e > s && e - s < (1ull << 31) ? (uint32_t)(e - s) : 0u;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t w[kBalGroups];
-        uint32_t sum = 0;
-        bool ok = grid >= kBalGroups && grid <= kBalMaxWg;
-#pragma unroll
-        for (uint32_t g = 0; g < kBalGroups; g++) {
-            sum += bl->hdr[1 + g];
-            ok = ok && bl->hdr[1 + g] > 0 && bl->span[g] > 0;
-        }
-        ok = ok && sum == kBalOne;
-        if (!ok) {
-#pragma unroll
-            for (uint32_t g = 0; g < kBalGroups; g++) w[g] = kBalOne / kBalGroups;
-        } else {
-            // rate of group g = its share / its time; move the weights by
-            // MCK_BAL_ALPHA towards the rate-proportional split
-            float r[kBalGroups], rs = 0.f, v[kBalGroups], vs = 0.f;
-#pragma unroll
-            for (uint32_t g = 0; g < kBalGroups; g++) {
-                r[g] = (float)bl->hdr[1 + g] / (float)bl->span[g];
-                rs += r[g];
-            }
-#pragma unroll
-            for (uint32_t g = 0; g < kBalGroups; g++) {
-                float x = (1.f - MCK_BAL_ALPHA) * (float)bl->hdr[1 + g] + MCK_BAL_ALPHA * (float)kBalOne * (r[g] / rs);
-                x = x < (float)(kBalOne / 32) ? (float)(kBalOne / 32) : x > (float)(kBalOne / 2) ? (float)(kBalOne / 2) : x;
-                v[g] = x;
-                vs += x;
-            }
-            uint32_t acc = 0;
-#pragma unroll
-            for (uint32_t g = 0; g + 1 < kBalGroups; g++) {
-                w[g] = (uint32_t)(v[g] / vs * (float)kBalOne);
-                acc += w[g];
-            }
-            w[kBalGroups - 1] = kBalOne - acc;
-        }
-        bl->cut[0] = 0;
-#pragma unroll
-        for (uint32_t g = 0; g < kBalGroups; g++) bl->cut[g + 1] = bl->cut[g] + w[g];
-        if (blockIdx.x == 0) {
-            BalBank *ob = a.bal + ((a.bal_seq + 1) & 1u);
-            ob->grid = gridDim.x;
-#pragma unroll
-            for (uint32_t g = 0; g < kBalGroups; g++) ob->w[g] = w[g];
-        }
-    }
-    __syncthreads();
 }
 
 // Exit counting of a launch that holds a slot, run by every wave once it has
@@ -622,7 +469,7 @@ __device__ __forceinline__ void slot_exit(unsigned long long *queue, uint32_t *w
 #endif
 template <bool DYN, class F>
 __device__ __forceinline__ bool for_each_unit(WgQueue *L, unsigned long long *queue, uint64_t n, uint32_t wave,
-                                              uint32_t nw, F &&body, const BalLds *bl = nullptr) {
+                                              uint32_t nw, F &&body) {
     if constexpr (DYN) {
         // One call site of body for both splits: a second inlined copy of the
         // payload loop made the offsets kernels spill, and so does the copy
@@ -742,57 +589,9 @@ __device__ __forceinline__ bool for_each_unit(WgQueue *L, unsigned long long *qu
         (void)nw;
         return __builtin_amdgcn_readfirstlane(first) != 0;
     } else {
-        // plain split: u = wave, wave + nw, ...; balanced (bl): see above.
-        // One call site of body for both.
-        (void)L;
-        (void)queue;
-        const uint32_t g = blockIdx.x % kBalGroups, wpb = blockDim.x / 64u;
-        const uint32_t nwg = (gridDim.x - g + kBalGroups - 1) / kBalGroups * wpb;  // waves of group g
-        const uint32_t lw = (blockIdx.x / kBalGroups) * wpb + (threadIdx.x >> 6);
-        const uint64_t S = (uint64_t)MCK_BAL_ROUND * nw;
-        const uint32_t c0 = bl ? __builtin_amdgcn_readfirstlane(bl->cut[g]) : 0u;
-        const uint32_t c1 = bl ? __builtin_amdgcn_readfirstlane(bl->cut[g + 1]) : 0u;
-        // group g's units, concatenated over the rounds, go to its waves in
-        // turn: wave lw takes the group's units lw, lw + nwg, ... -- so a
-        // share that is not a multiple of the group's waves spreads its surplus
-        // over all waves instead of piling it on the first few of every round.
-        // k indexes the group's units from the round at `base` on ([lo, hi)).
-        uint64_t base = 0, lo = 0, hi = n, k = lw;
-        auto settle = [&]() -> uint64_t {
-            for (; base < n; base += S) {
-                const uint64_t size = n - base < S ? n - base : S;
-                lo = base + ((size * c0) >> 24);
-                hi = base + ((size * c1) >> 24);
-                if (k < hi - lo) return lo + k;
-                k -= hi - lo;
-            }
-            return n;
-        };
-        uint64_t u = bl ? settle() : wave;
-        while (u < n) {
-            body(u);
-            if (bl) {
-                k = u - lo + nwg;
-                u = settle();
-            } else {
-                u += nw;
-            }
-        }
+        for (uint64_t u = wave; u < n; u += nw) body(u);
         return false;
     }
-}
-
-// After a balanced launch's units (every wave): exit counting on the slot;
-// the last wave of each workgroup records the workgroup's entry and exit
-// stamps for the next launch.
-__device__ __forceinline__ void bal_exit(const BatchArgs &a, BalLds *bl) {
-    slot_exit(a.queue, &bl->exited, [&] {
-        if ((threadIdx.x & 63u) == 0 && blockIdx.x < kBalMaxWg) {
-            BalBank *ob = a.bal + ((a.bal_seq + 1) & 1u);
-            ob->rec[2 * blockIdx.x] = bl->start;
-            ob->rec[2 * blockIdx.x + 1] = wall_clock64();
-        }
-    });
 }
 
 // Run by the wave for_each_unit picked after a give-up (wave-uniform): the
@@ -1160,6 +959,29 @@ __device__ __forceinline__ uint32_t payload32_generic(TAB lds, const crc32_gpu_p
     return x;
 }
 
+// Step grid of the one-payload-per-wave loops (payload32_g64 / payload64_g64):
+// the window of 1 KiB steps ENDS on a 128-B line boundary past the payload
+// (MCK_ALIGN128; 16 B before round 3), so every step reads exactly 8 whole
+// lines.  With non-temporal loads a line that two steps straddle is fetched
+// twice: on C4's byte-packed payloads that was 1.7% of extra HBM requests
+// (TCC_EA0_RDREQ: 6.83e7 vs 6.74e7 with NT off, profiles/r03/tcc_c4_nt*.txt;
+// NT off costs 11%).  Reads stay inside the last byte's 128-B line, hence
+// its page.  The up-to-127 pad bytes are removed by Z^-t, t = 16q + r: the
+// tail table Z^-r and the butterfly operators Z^-(16*2^k) for the bits of q.
+#ifndef MCK_ALIGN128
+#define MCK_ALIGN128 1
+#endif
+constexpr uint64_t kGridAlign = MCK_ALIGN128 ? 128 : 16;
+
+template <class TAB>
+__device__ __forceinline__ uint32_t tail32(TAB lds, uint32_t t, uint32_t x) {
+    x = op32(lds, 2 + 6 + (t & 15u), x);
+#pragma unroll
+    for (uint32_t k = 0; k < 3; k++)
+        if ((t >> (4 + k)) & 1u) x = op32(lds, 2 + k, x);
+    return x;
+}
+
 // One payload per wave (G = 64): the window geometry is wave-uniform, so the
 // payload base stays in SGPRs, each lane carries a 32-bit offset (saddr-form
 // global loads), and "does this step touch an edge?" is a scalar test -- only
@@ -1171,7 +993,7 @@ __device__ __forceinline__ uint32_t payload32_g64(TAB lds, const crc32_gpu_pack_
                                                   uint64_t len, uint32_t gl, uint32_t lc0, uint32_t lc1) {
     const uint32_t init = RAW ? 0u : pk->init;
     const uint64_t sa = reinterpret_cast<uint64_t>(p), ea = sa + len;
-    const uint64_t a0 = sa & ~15ull, a1 = (ea + 15) & ~15ull;
+    const uint64_t a0 = sa & ~15ull, a1 = (ea + kGridAlign - 1) & ~(kGridAlign - 1);
     const uint32_t W = (uint32_t)(a1 - a0);
     const uint32_t K = (W + 1023u) >> 10;
     const uint32_t lead = K * 1024u - W;                 // window starts `lead` bytes into step 0
@@ -1225,7 +1047,7 @@ __device__ __forceinline__ uint32_t payload32_g64(TAB lds, const crc32_gpu_pack_
         }
     }
     uint32_t x = combine32<6>(lds, x0, x1, x2, x3, gl);
-    x = op32(lds, 2 + 6 + (uint32_t)(a1 - ea), x);
+    x = tail32(lds, (uint32_t)(a1 - ea), x);
     if (!RAW && len < 4) x ^= pk->zinit[len];
     return x;
 }
@@ -1310,17 +1132,8 @@ __global__ __launch_bounds__(kBlk32<LIGHT>, 1) void crc32c_batch_kernel(BatchArg
     if (!DYN) return;  // diagnostic: launch cost alone
 #endif
     if (DYN && threadIdx.x == 0) wg_queue_init(&wgq, a.queue, units);
-    // feedback-balanced static split (the host passes a record only for
-    // eager launches with a slot, >= 8 and <= kBalMaxWg workgroups)
-    constexpr bool kBal = MCK_BAL && !DYN && !LIGHT && MODE == kFixedAligned;
-    __shared__ BalLds bl;
-    const bool bal = kBal && a.bal != nullptr;
-    BalPre bp{};
-    if (bal) bp = bal_prefetch(a, &bl);
     fill_lds32<LIGHT, kBlk32<LIGHT>>(lds_raw, pk);
-    if (bal) bal_stash(&bl, bp);
     __syncthreads();
-    if (bal) bal_plan(a, &bl, bp);
 #if defined(MCK_EMPTY) && MCK_EMPTY == 1
     if (!DYN) return;  // diagnostic: launch + LDS table fill
 #endif
@@ -1373,9 +1186,8 @@ __global__ __launch_bounds__(kBlk32<LIGHT>, 1) void crc32c_batch_kernel(BatchArg
         else
             x = payload32_generic<LOG2G, NT>(lds, pk, a.base + pc * a.stride, a.len, gl, lc0, lc1);
         if (act && gl == 0) emit<uint32_t, VERIFY>(a, p, x ^ xorout);
-    }, bal ? &bl : nullptr);
+    });
     if (faulted) fail_closed<VERIFY>(a);
-    if (bal) bal_exit(a, &bl);
     MCK_STAMP(wave, 2);
 }
 
@@ -1655,7 +1467,7 @@ template <int LOG2G, bool NT, bool OG>
 __device__ __forceinline__ uint64_t payload64_aligned(const uint8_t *lds, const crc64_gpu_pack_t *pk, const uint8_t *p,
                                                       uint32_t K, uint32_t gl, uint32_t lc, uint64_t init) {
     constexpr int G = 1 << LOG2G;
-    constexpr int R = kRing;
+    constexpr int R = MCK_RING64;
     Lane64 ln = lane64(lc);
     // global (address-space 1) loads: a flat load would also hold up every LDS wait
     const gbyte_t src = global_ptr(p, LOG2G == 6) + 16u * gl;
@@ -1765,13 +1577,22 @@ __device__ __forceinline__ uint64_t payload64_generic(const uint8_t *lds, const 
     return x;
 }
 
+template <int OM>
+__device__ __forceinline__ uint64_t tail64(const uint8_t *lds, const crc64_gpu_pack_t *pk, uint32_t t, uint64_t x) {
+    x = opm64<OM>(lds, pk, 1 + 6 + (t & 15u), x);
+#pragma unroll
+    for (uint32_t k = 0; k < 3; k++)
+        if ((t >> (4 + k)) & 1u) x = opm64<OM>(lds, pk, 1 + k, x);
+    return x;
+}
+
 // CRC-64 counterpart of payload32_g64.
 template <bool NT, bool RAW = false, int OM = kOpsLds>
 __device__ __forceinline__ uint64_t payload64_g64(const uint8_t *lds, const crc64_gpu_pack_t *pk, const uint8_t *p,
                                                   uint64_t len, uint32_t gl, uint32_t lc) {
     const uint64_t init = RAW ? 0ull : pk->init;
     const uint64_t sa = reinterpret_cast<uint64_t>(p), ea = sa + len;
-    const uint64_t a0 = sa & ~15ull, a1 = (ea + 15) & ~15ull;
+    const uint64_t a0 = sa & ~15ull, a1 = (ea + kGridAlign - 1) & ~(kGridAlign - 1);
     const uint32_t W = (uint32_t)(a1 - a0);
     const uint32_t K = (W + 1023u) >> 10;
     const uint32_t lead = K * 1024u - W;
@@ -1818,7 +1639,7 @@ __device__ __forceinline__ uint64_t payload64_g64(const uint8_t *lds, const crc6
         }
     }
     uint64_t x = combine64<6, OM>(lds, pk, x0, x1, gl);
-    x = opm64<OM>(lds, pk, 1 + 6 + (uint32_t)(a1 - ea), x);
+    x = tail64<OM>(lds, pk, (uint32_t)(a1 - ea), x);
     if (!RAW && len < 8) x ^= pk->zinit[len];
     return x;
 }
@@ -1842,17 +1663,8 @@ __global__ __launch_bounds__(kBlk64<MODE>, kWpe64<MODE>) void crc64_batch_kernel
     constexpr bool DYN = dyn_policy(64, MODE, NT, false) || SPLIT;
     MCK_STAMP(blockIdx.x * kWPB + (threadIdx.x >> 6), 0);
     if (DYN && threadIdx.x == 0) wg_queue_init(&wgq, a.queue, units);
-    // (off by default: the split's state pushed the 64-VGPR static CRC-64
-    // kernels into 13-18 VGPR spills)
-    constexpr bool kBal = MCK_BAL && MCK_BAL64 && !DYN && MODE == kFixedAligned;
-    __shared__ BalLds bl;
-    const bool bal = kBal && a.bal != nullptr;
-    BalPre bp{};
-    if (bal) bp = bal_prefetch(a, &bl);
     fill_lds64<S::block, S::ops_mode>(lds, pk);
-    if (bal) bal_stash(&bl, bp);
     __syncthreads();
-    if (bal) bal_plan(a, &bl, bp);
     MCK_STAMP(blockIdx.x * kWPB + (threadIdx.x >> 6), 1);
 
     const uint32_t lane = threadIdx.x & 63u;
@@ -1907,9 +1719,8 @@ __global__ __launch_bounds__(kBlk64<MODE>, kWpe64<MODE>) void crc64_batch_kernel
         else
             x = payload64_generic<LOG2G, NT>(lds, pk, a.base + pc * a.stride, a.len, gl, lc);
         if (act && gl == 0) emit<uint64_t, VERIFY>(a, p, x ^ xorout);
-    }, bal ? &bl : nullptr);
+    });
     if (faulted) fail_closed<VERIFY>(a);
-    if (bal) bal_exit(a, &bl);
     MCK_STAMP(blockIdx.x * kWPB + (threadIdx.x >> 6), 2);
 }
 

@@ -20,14 +20,12 @@ constexpr int kMaxDev = 64;
 constexpr uint32_t kStreamSlots = 2048;
 constexpr uint32_t kQueueSlots = kStreamSlots;
 
-// One slot: the work-queue counters (kQSlotWords words in DevCtx::queue) and
-// the balanced split's record (two BalBanks in DevCtx::bal), owned by one
-// stream at a time.
+// One slot: the work-queue counters (kQSlotWords words in DevCtx::queue),
+// owned by one stream at a time.
 struct SlotState {
     uintptr_t sid = 0;  // owning stream (handle)
     uint64_t issued = 0;         // launches handed this slot (the kernels count completions, kQDone)
     uint64_t last_use = 0;       // LRU tick
-    uint32_t bal_seq = 0;        // balanced launches on the slot (bank parity)
     bool owned = false;
 };
 
@@ -45,7 +43,6 @@ struct DevCtx {
     // Graph-captured launches, and streams that find no idle slot, get none
     // and take the plain static split (crc_gpu_device.h, "Exclusivity").
     unsigned long long *queue = nullptr;
-    void *bal = nullptr;                        // kQueueSlots x 2 BalBanks
     SlotState slot[kQueueSlots];               // guarded by g_mu
     std::unordered_map<uintptr_t, uint32_t> sid_slot;  // guarded by g_mu
     uint32_t nslots = 0;                        // slots handed out so far
@@ -56,11 +53,9 @@ struct DevCtx {
     long long n_slot = 0, n_noslot = 0, n_reclaim = 0, n_busy_skip = 0;
 };
 
-// A launch's slot: counters, balance record and its sequence on that record.
+// A launch's slot (counters) and its index.
 struct SlotRef {
     unsigned long long *q = nullptr;
-    void *bal = nullptr;  // the slot's two BalBanks (crc_gpu_device.h)
-    uint32_t seq = 0;
     int idx = -1;
 };
 
@@ -87,11 +82,10 @@ int prologue(const char *method, int log2g, int *width, DevCtx **c, const void *
 int get_ext(DevCtx *c, int idx, const void **out);
 // Work-queue slot for one launch of a throughput (non-light) batch kernel on
 // `stream`, exclusive to that stream; empty (static split) for a launch being
-// captured into a graph or a stream that finds no idle slot.  `bal`: the
-// launch uses the balance record (takes a sequence number on it).  Every
-// launch given a slot must count itself done on it (slot_exit): if the launch
-// fails to start, slot_unissue() takes the launch back.
-SlotRef queue_slot(DevCtx *c, void *stream, bool bal = false);
+// captured into a graph or a stream that finds no idle slot.  Every launch
+// given a slot must count itself done on it (slot_exit): if the launch fails
+// to start, slot_unissue() takes the launch back.
+SlotRef queue_slot(DevCtx *c, void *stream);
 void slot_unissue(DevCtx *c, const SlotRef &r);
 // Queue-fault count of mchecksum_gpu_ext.hip's kernels (their own copy of
 // g_mck_queue_faults) on the current device; -1 on error.

@@ -128,19 +128,14 @@ int device_ctx(DevCtx **out) {
         if (e != hipSuccess) return hip_err(e, "hipDeviceGetAttribute");
         c.cus = cus > 0 ? cus : 1;
         const size_t qbytes = (size_t)kQueueSlots * kQSlotWords * sizeof(unsigned long long);
-        const size_t bbytes = (size_t)kQueueSlots * 2 * sizeof(BalBank);
         e = hipMalloc(reinterpret_cast<void **>(&c.queue), qbytes);
         if (e == hipSuccess) e = hipMemset(c.queue, 0, qbytes);
-        if (e == hipSuccess) e = hipMalloc(&c.bal, bbytes);
-        if (e == hipSuccess) e = hipMemset(c.bal, 0, bbytes);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&c.probe, hipStreamNonBlocking);
         if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&c.probe_host), sizeof(unsigned long long));
         if (e != hipSuccess) {
             if (c.queue) (void)hipFree(c.queue);
-            if (c.bal) (void)hipFree(c.bal);
             if (c.probe) (void)hipStreamDestroy(c.probe);
             c.queue = nullptr;
-            c.bal = nullptr;
             c.probe = nullptr;
             return hip_err(e, "work-queue allocation");
         }
@@ -187,26 +182,20 @@ int get_pack(DevCtx *c, int idx, int log2g, const void **pack) {
     return 0;
 }
 
-// Launches slot i has completed (its kernels' kQDone counter), read on the
-// private stream; -1 if the read fails (caller holds g_mu).
-long long slot_done(DevCtx *c, uint32_t i) {
+// Whether slot i has completed every launch it was issued (its kernels'
+// kQDone counter, read on the private stream); false if the read fails
+// (caller holds g_mu).
+bool slot_idle(DevCtx *c, uint32_t i) {
     if (hipMemcpyAsync(c->probe_host, c->queue + (size_t)i * kQSlotWords + kQDone * kQStride,
                        sizeof(unsigned long long), hipMemcpyDeviceToHost, c->probe) != hipSuccess ||
         hipStreamSynchronize(c->probe) != hipSuccess) {
         (void)hipGetLastError();
-        return -1;
+        return false;
     }
-    return (long long)*c->probe_host;
+    return *c->probe_host == c->slot[i].issued;
 }
 
-// Balanced split off (MCHECKSUM_GPU_BAL=0): every static launch takes the
-// plain split without a slot (A/B switch, read per call like the other knobs).
-bool bal_enabled() {
-    const char *env = getenv("MCHECKSUM_GPU_BAL");
-    return !(env && env[0] == '0');
-}
-
-SlotRef queue_slot(DevCtx *c, void *stream, bool bal) {
+SlotRef queue_slot(DevCtx *c, void *stream) {
     SlotRef r;
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing((hipStream_t)stream, &st) != hipSuccess) {
@@ -216,7 +205,7 @@ SlotRef queue_slot(DevCtx *c, void *stream, bool bal) {
     // A captured launch replays with these arguments, possibly on two graph
     // execs at once: no exclusive slot exists for it, so it takes the static
     // split (crc_gpu_device.h, "Exclusivity").
-    if (st != hipStreamCaptureStatusNone || (bal && !bal_enabled())) {
+    if (st != hipStreamCaptureStatusNone) {
         std::lock_guard<std::mutex> lk(g_mu);
         c->n_noslot++;
         return r;
@@ -264,7 +253,7 @@ SlotRef queue_slot(DevCtx *c, void *stream, bool bal) {
         }
         i = kQueueSlots;
         for (uint32_t k = 0; k < nc && i == kQueueSlots; k++) {
-            if (slot_done(c, cand[k]) == (long long)c->slot[cand[k]].issued) i = cand[k];
+            if (slot_idle(c, cand[k])) i = cand[k];
             else c->n_busy_skip++;
         }
         if (i == kQueueSlots) {
@@ -285,19 +274,13 @@ SlotRef queue_slot(DevCtx *c, void *stream, bool bal) {
     c->n_slot++;
     r.q = c->queue + (size_t)i * kQSlotWords;
     r.idx = (int)i;
-    if (bal) {
-        r.bal = static_cast<BalBank *>(c->bal) + 2 * (size_t)i;
-        r.seq = s.bal_seq++;
-    }
     return r;
 }
 
 void slot_unissue(DevCtx *c, const SlotRef &r) {
     if (r.idx < 0) return;
     std::lock_guard<std::mutex> lk(g_mu);
-    SlotState &s = c->slot[r.idx];
-    s.issued--;
-    if (r.bal) s.bal_seq--;
+    c->slot[r.idx].issued--;
 }
 
 uint32_t *error_word() { return t_err_word; }
@@ -551,13 +534,6 @@ int launch_fixed(DevCtx *c, int idx, const void *pack, int width, int lg, const 
     if (dyn) {
         sr = queue_slot(c, stream);
         a.queue = sr.q;
-    } else if (MCK_BAL && (width == 32 || MCK_BAL64) && aligned && !light && blocks >= kBalGroups && blocks <= kBalMaxWg &&
-               units >= (uint64_t)blocks * (uint64_t)(k.block / 64)) {
-        // the balanced static split (crc_gpu_device.h): a full grid only
-        sr = queue_slot(c, stream, true);
-        a.queue = sr.q;
-        a.bal = static_cast<BalBank *>(sr.bal);
-        a.bal_seq = sr.seq;
     }
     int rc = launch(k, a, blocks, stream);
     if (rc != MCHECKSUM_GPU_OK) slot_unissue(c, sr);
@@ -718,16 +694,6 @@ MCHECKSUM_PUBLIC int mck_debug_units_read(void *host, size_t bytes) {
 MCHECKSUM_PUBLIC int mck_debug_trace_xcc_read(void *host, size_t bytes) {
     if (bytes > sizeof(g_mck_trace_xcc)) bytes = sizeof(g_mck_trace_xcc);
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_mck_trace_xcc), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
-}
-// ... the balanced split's two banks of slot `slot` on the current device ...
-MCHECKSUM_PUBLIC int mck_debug_bal_read(int slot, void *host, size_t bytes) {
-    DevCtx *c = nullptr;
-    {
-        std::lock_guard<std::mutex> lk(g_mu);
-        if (device_ctx(&c) || slot < 0 || slot >= (int)kQueueSlots) return -1;
-    }
-    if (bytes > 2 * sizeof(BalBank)) bytes = 2 * sizeof(BalBank);
-    return hipMemcpy(host, static_cast<BalBank *>(c->bal) + 2 * (size_t)slot, bytes, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
 // ... and the work-queue fault records (count, then 4 words per record).
 MCHECKSUM_PUBLIC int mck_debug_qdiag_read(unsigned int *n, unsigned long long *rec) {

@@ -35,12 +35,21 @@ static T raw_word(const uint8_t *buf, int64_t nbuf, int64_t wa) {
     return w;
 }
 
+// End of the step grid: the payload's end rounded up to 16 B, or -- with
+// EMU_GRID_ALIGN=128, the one-payload-per-wave loops (G = 64) of round 3 --
+// to the 128-B line, so every step covers whole lines.
+static int64_t grid_end(int64_t end, int log2g) {
+    const char *e = getenv("EMU_GRID_ALIGN");
+    const int64_t al = log2g == 6 && e && atoi(e) == 128 ? 128 : 16;
+    return (end + al - 1) & ~(al - 1);
+}
+
 // CRC of payload buf[start, start+len) as the kernel computes it.
 extern "C" uint32_t emu_crc32(const crc32_gpu_pack_t *pk, const uint8_t *buf, int64_t nbuf, int64_t start,
                               int64_t len) {
     const int log2g = (int)pk->log2g, G = 1 << log2g;
     const int64_t step = 16LL * G;
-    int64_t a0 = start & ~15LL, a1 = (start + len + 15) & ~15LL, t = a1 - (start + len);
+    int64_t a0 = start & ~15LL, a1 = grid_end(start + len, log2g), t = a1 - (start + len);
     int64_t W = a1 - a0, K = (W + step - 1) / step, r0 = W - K * step;
     int64_t hs = start - a0, he = start + len - a0;
     std::vector<uint32_t> S(4 * G, 0);
@@ -90,7 +99,10 @@ extern "C" uint32_t emu_crc32(const crc32_gpu_pack_t *pk, const uint8_t *buf, in
             X = Y;
         }
     }
-    uint32_t r = op32(*pk, 2 + log2g + (int)t, X[0]);
+    // pad undo Z^-t, t = 16q + r (q > 0 only on the 128-B grid, G = 64)
+    uint32_t r = op32(*pk, 2 + log2g + (int)(t & 15), X[0]);
+    for (int k = 0; k < 3; k++)
+        if ((t >> (4 + k)) & 1) r = op32(*pk, 2 + k, r);
     if (len < 4) r ^= pk->zinit[len];
     return r ^ pk->xorout;
 }
@@ -99,7 +111,7 @@ extern "C" uint64_t emu_crc64(const crc64_gpu_pack_t *pk, const uint8_t *buf, in
                               int64_t len) {
     const int log2g = (int)pk->log2g, G = 1 << log2g;
     const int64_t step = 16LL * G;
-    int64_t a0 = start & ~15LL, a1 = (start + len + 15) & ~15LL, t = a1 - (start + len);
+    int64_t a0 = start & ~15LL, a1 = grid_end(start + len, log2g), t = a1 - (start + len);
     int64_t W = a1 - a0, K = (W + step - 1) / step, r0 = W - K * step;
     int64_t hs = start - a0, he = start + len - a0;
     std::vector<uint64_t> S(2 * G, 0);
@@ -138,7 +150,9 @@ extern "C" uint64_t emu_crc64(const crc64_gpu_pack_t *pk, const uint8_t *buf, in
         }
         X = Y;
     }
-    uint64_t r = op64(*pk, 1 + log2g + (int)t, X[0]);
+    uint64_t r = op64(*pk, 1 + log2g + (int)(t & 15), X[0]);
+    for (int k = 0; k < 3; k++)
+        if ((t >> (4 + k)) & 1) r = op64(*pk, 1 + k, r);
     if (len < 8) r ^= pk->zinit[len];
     return r ^ pk->xorout;
 }
@@ -191,6 +205,41 @@ int main() {
                 n++;
                 if (e != g) { fails++; if (fails < 10) printf("crc64-ecma182 lg=%d len=%ld start=%ld %016lx vs %016lx\n", lg, (long)len, (long)start, (unsigned long)g, (unsigned long)e); }
             }
+    }
+    // MSB-first models with non-zero init and/or xorout (not in the product
+    // catalogue): their init and xorout map into the byte-reversed
+    // register domain exactly as mchecksum_gpu.hip's gpu_rmodel does --
+    // rinit = R(reflect(init)), xorout = R(reflect(xorout)).  Catalogue
+    // check values pin the synthetic models themselves.
+    static const oracle_model_t msbz[] = {
+        {"crc64-we", 64, 0x42F0E1EBA9EA3693ULL, 0, 0, ~0ULL, ~0ULL, 0x62EC59E3F1A4F00AULL},
+        {"crc32-bzip2", 32, 0x04C11DB7ULL, 0, 0, 0xFFFFFFFFULL, 0xFFFFFFFFULL, 0xFC891918ULL},
+        {"crc32-mpeg2", 32, 0x04C11DB7ULL, 0, 0, 0xFFFFFFFFULL, 0ULL, 0x0376E6E7ULL},
+    };
+    for (const oracle_model_t &mm : msbz) {
+        if (oracle_crc_bitwise(&mm, "123456789", 9) != mm.check) {
+            fails++;
+            printf("%s: check value differs\n", mm.name);
+            continue;
+        }
+        const int w = mm.width;
+        crc_rmodel_t rm = {w, refl(mm.poly, w), crc_rev_bytes(w, refl(mm.init, w)), crc_rev_bytes(w, refl(mm.xorout, w)), 1};
+        for (int lg : {0, 3, 6}) {
+            static crc32_gpu_pack_t q32;
+            static crc64_gpu_pack_t q64;
+            if (w == 32 ? crc32_gpu_pack_build(&rm, lg, &q32) : crc64_gpu_pack_build(&rm, lg, &q64)) {
+                printf("%s pack build failed\n", mm.name);
+                return 1;
+            }
+            for (int64_t len : {0, 1, 3, 4, 5, 7, 8, 9, 63, 64, 65, 1023, 1024, 4097, 65536})
+                for (int64_t start : {0, 1, 5, 8, 13, 16}) {
+                    const uint64_t e = oracle_crc_table(&mm, buf.data() + start, len);
+                    const uint64_t g = w == 32 ? __builtin_bswap32(emu_crc32(&q32, buf.data(), (int64_t)buf.size(), start, len))
+                                               : __builtin_bswap64(emu_crc64(&q64, buf.data(), (int64_t)buf.size(), start, len));
+                    n++;
+                    if (e != g) { fails++; if (fails < 10) printf("%s lg=%d len=%ld start=%ld %016lx vs %016lx\n", mm.name, lg, (long)len, (long)start, (unsigned long)g, (unsigned long)e); }
+                }
+        }
     }
     printf("%d cases, %d failures\n", n, fails);
     return fails != 0;

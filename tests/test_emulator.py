@@ -56,3 +56,21 @@ def test_emulated_kernel_equals_oracle(emu, oracle_mod, log2g):
         d = buf[start:start + n]
         assert emu.emu_crc32(p32, buf.ctypes.data, buf.size, start, n) == oracle_mod.crc("crc32c", d), (start, n)
         assert emu.emu_crc64(p64, buf.ctypes.data, buf.size, start, n) == oracle_mod.crc("crc64", d), (start, n)
+
+
+@pytest.mark.parametrize("log2g", [6])
+def test_emulated_128b_grid_equals_oracle(emu, oracle_mod, log2g, monkeypatch):
+    """The one-payload-per-wave loops end their step grid on a 128-B line
+    (round 3, crc_gpu_device.h kGridAlign): up to 127 pad bytes, undone by the
+    tail table and the butterfly operators.  Every start alignment and lengths
+    around each multiple of 16 and 128."""
+    monkeypatch.setenv("EMU_GRID_ALIGN", "128")
+    p32, p64 = emu.emu_pack32(log2g), emu.emu_pack64(log2g)
+    buf = oracle_mod.splitmix_bytes(140000, 0x128)
+    lens = sorted({0, 1, 3, 4, 7, 8, 9, 15, 16, 17} | {m + d for m in (127, 128, 255, 256, 1024, 1151, 4096, 65536)
+                                                        for d in (-1, 0, 1)})
+    for start in list(range(0, 130, 7)) + [1023, 4097]:
+        for n in lens:
+            d = buf[start:start + n]
+            assert emu.emu_crc32(p32, buf.ctypes.data, buf.size, start, n) == oracle_mod.crc("crc32c", d), (start, n)
+            assert emu.emu_crc64(p64, buf.ctypes.data, buf.size, start, n) == oracle_mod.crc("crc64", d), (start, n)

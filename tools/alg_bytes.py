@@ -14,6 +14,9 @@ method, count, length, seed = SHAPES[sys.argv[1]]
 w = 4 if method == "crc32c" else 8
 if sys.argv[1] == "msgs":  # messages read (headers included), 1 status byte each, the offsets table
     print(int(varlen_offsets(seed, count)[-1]) + count + 8 * (count + 1))
+elif sys.argv[1] == "xdr":  # XDR messages read, output CRCs, the offsets table
+    import bench
+    print(int(bench.xdr_offsets(seed, count)[-1]) + w * count + 8 * (count + 1))
 elif sys.argv[1] == "seg":  # bulk-segment layout: + segment table (addr, len) and object index
     print(count * length + w * count + 16 * 4 * count + 8 * (count + 1))
 elif length is None:

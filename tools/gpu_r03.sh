@@ -1,8 +1,9 @@
 #!/bin/bash
 # Round-3 GPU passes.  PART selects one:
 #   tests  -- new slot / fail-closed tests first, then the whole -m gpu suite
-#   ab     -- in-process A/B: working tree (cur) vs last commit (prev) and the
-#             balanced split switched off (BALOFF) on AB_CONFIGS
+#   ab     -- in-process A/B (tools/ab_variants.py): AB_VARIANTS of build/variants
+#             (default: working tree "cur" vs last commit "prev") plus the
+#             env pseudo-variants in AB_ENV, on AB_CONFIGS
 #   bench  -- bench.py per CONFIGS into gpurun_out/r03/bench_<config>.json
 #   trace  -- rocprofv3 kernel-trace summaries of bench.py per CONFIGS
 #   pmc    -- FETCH_SIZE / WRITE_SIZE passes per CONFIGS -> pmc_traffic_<config>.json
@@ -28,9 +29,16 @@ fi
 if [ "$P" = ab ]; then
   step "ab ${AB_CONFIGS:-c2,metric}"
   timeout -k 10 600 python tools/ab_variants.py --config ${AB_CONFIGS:-c2,metric} --variants ${AB_VARIANTS:-prev cur} \
-    ${AB_ENV:---env BALOFF=MCHECKSUM_GPU_BAL=0} --rounds ${AB_ROUNDS:-6} --iters ${AB_ITERS:-10} \
+    ${AB_ENV:-} --rounds ${AB_ROUNDS:-6} --iters ${AB_ITERS:-10} \
     --out $O/ab_${AB_TAG:-r03}.json > $O/ab_${AB_TAG:-r03}.log 2>&1; rc=$?
   grep -v amdgpu.ids $O/ab_${AB_TAG:-r03}.log; [ $rc -eq 0 ] || exit $rc
+fi
+if [ "$P" = xdrtest ]; then
+  step "xdr tests"
+  timeout -k 10 600 python -u -m pytest tests/test_xdr.py -m gpu -x -v --timeout 300 --timeout-method thread \
+    > $O/pytest_xdr.log 2>&1; rc=$?
+  tail -5 $O/pytest_xdr.log
+  [ $rc -eq 0 ] || { grep -E "Error|assert|FAILED|^E " $O/pytest_xdr.log | head -60; exit $rc; }
 fi
 if [ "$P" = bench ]; then
   for c in ${CONFIGS:-metric c2}; do
@@ -59,7 +67,8 @@ if [ "$P" = pmc ]; then
     step "pmc $c"
     timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/tr_${c}_f -o p -- python3 $R/tools/kernel_run.py --config $c --iters 4 > $O/tr_${c}_f.log 2>&1 || { tail $O/tr_${c}_f.log; exit 1; }
     timeout -k 10 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/tr_${c}_w -o p -- python3 $R/tools/kernel_run.py --config $c --iters 4 > $O/tr_${c}_w.log 2>&1 || { tail $O/tr_${c}_w.log; exit 1; }
-    python3 $R/tools/pmc_traffic.py $O/tr_${c}_f $O/tr_${c}_w batch_kernel $O/pmc_traffic_$c.json $(python3 $R/tools/alg_bytes.py $c) 1 4 || exit 1
+    k=batch_kernel; [ "$c" = xdr ] && k=xdr_fast_kernel
+    python3 $R/tools/pmc_traffic.py $O/tr_${c}_f $O/tr_${c}_w $k $O/pmc_traffic_$c.json $(python3 $R/tools/alg_bytes.py $c) 1 4 || exit 1
   done
   cd "$R"
 fi

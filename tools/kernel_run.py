@@ -29,6 +29,18 @@ if a.config == "msgs":  # bench.py's msgs layout: HG header (network-order paylo
     status = torch.empty(count, dtype=torch.uint8, device="cuda")
     mism = torch.zeros(1, dtype=torch.int32, device="cuda")
     run = lambda: G.verify_messages(data, offs, status=status, mismatches=mism)
+elif a.config == "xdr":  # bench.py's xdr layout: hg_perf_proc_iovec messages in XDR mode
+    import bench
+    from mercury_amd.workload import varlen_lengths
+    off = bench.xdr_offsets(seed, count)
+    lens = torch.from_numpy(varlen_lengths(seed, count).astype(np.int64)).cuda()
+    data = torch.empty(int(off[-1]) + 64, dtype=torch.uint8, device="cuda")
+    G.fill_splitmix(data, seed)
+    offs = torch.from_numpy(off.astype(np.int64)).cuda()
+    for k in range(4):
+        data[offs[:-1] + k] = ((lens >> (24 - 8 * k)) & 0xFF).to(torch.uint8)
+    xout = torch.empty(count, dtype=torch.int32, device="cuda")
+    run = lambda: G.checksum_xdr(method, data, offs, bench.XDR_IOVEC, out=xout)
 elif length is None:
     from mercury_amd.workload import varlen_offsets
     off = varlen_offsets(seed, count)

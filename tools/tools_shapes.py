@@ -6,4 +6,5 @@ SHAPES = {
     "c4": ("crc32c", 262144, None, 0x4D43310000000004),
     "c5": ("crc32c", 1 << 20, 65536, 0x4D43310000000005),
     "msgs": ("crc32c", 262144, None, 0x4D43310000000004),   # C4's packets as Mercury messages, verified
+    "xdr": ("crc32c", 262144, None, 0x4D43310000000004),    # C4's payloads as XDR iovec messages
 }
