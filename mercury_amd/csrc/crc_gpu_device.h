@@ -430,6 +430,9 @@ __device__ __forceinline__ T wave_max(T v) {
 // workgroup runs wg_last() and counts in its group's line, the last workgroup
 // of a group in the slot's line; the last group zeroes the slot's protocol
 // lines for the next launch and then, after a fence, counts the launch done.
+#ifndef MCK_SLOT_FENCE
+#define MCK_SLOT_FENCE 0
+#endif
 template <class F>
 __device__ __forceinline__ void slot_exit(unsigned long long *queue, uint32_t *wg_exited, F &&wg_last) {
     const bool l0 = (threadIdx.x & 63u) == 0;
@@ -449,7 +452,15 @@ __device__ __forceinline__ void slot_exit(unsigned long long *queue, uint32_t *w
     if (__builtin_amdgcn_readfirstlane(last)) {  // one instruction: lane j zeroes line j
         const uint32_t j = threadIdx.x & 63u;
         if (j < kQSlotLines) atomicExch(queue + j * kQStride, 0ull);
+        // The done count must not land before the zeroing: wait until this
+        // wave's atomics have been performed (vmcnt also counts stores and
+        // non-returning atomics on gfx9-family parts).  An agent-scope fence
+        // would also write back the whole L2 (buffer_wbl2).
+#if MCK_SLOT_FENCE
         __threadfence();
+#else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
         if (j == 0) atomicAdd(queue + kQDone * kQStride, 1ull);
     }
 }
