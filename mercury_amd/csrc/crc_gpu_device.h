@@ -997,12 +997,16 @@ __device__ __forceinline__ uint32_t tail32(TAB lds, uint32_t t, uint32_t x) {
 // payload base stays in SGPRs, each lane carries a 32-bit offset (saddr-form
 // global loads), and "does this step touch an edge?" is a scalar test -- only
 // the first/last steps pay for per-lane masking.  Payloads < 2 GiB.
-// RAW: init 0 and no finalisation -- the linear part L(M) of the CRC (used to
-// combine the pieces of a scatter-gather object, mchecksum_gpu_ext.hip).
+// RAW: no finalisation and the register starts at `reg` (default 0: the
+// linear part L(M) of the CRC, used to combine the pieces of a scatter-gather
+// object, mchecksum_gpu_ext.hip); a non-zero `reg` continues a running
+// register (the XDR walker's fields) and needs len >= 4, since it rides in
+// the first four payload bytes (R(reg, M) = R(0, M ^ reg)).
 template <bool NT, class TAB, bool RAW = false>
 __device__ __forceinline__ uint32_t payload32_g64(TAB lds, const crc32_gpu_pack_t *pk, const uint8_t *p,
-                                                  uint64_t len, uint32_t gl, uint32_t lc0, uint32_t lc1) {
-    const uint32_t init = RAW ? 0u : pk->init;
+                                                  uint64_t len, uint32_t gl, uint32_t lc0, uint32_t lc1,
+                                                  uint32_t reg = 0u) {
+    const uint32_t init = RAW ? reg : pk->init;
     const uint64_t sa = reinterpret_cast<uint64_t>(p), ea = sa + len;
     const uint64_t a0 = sa & ~15ull, a1 = (ea + kGridAlign - 1) & ~(kGridAlign - 1);
     const uint32_t W = (uint32_t)(a1 - a0);
@@ -1095,6 +1099,9 @@ constexpr int kTraceWaves = 16384;
 __device__ unsigned long long g_mck_trace[3 * kTraceWaves];
 // the XCD each wave ran on (hardware register XCC_ID), stamped at entry
 __device__ unsigned int g_mck_trace_xcc[kTraceWaves];
+// the shader-clock counter (clock64) at entry and exit: with the wall stamps
+// the clock each XCD ran at over the wave's life (tools/xcd_clock.py)
+__device__ unsigned long long g_mck_trace_clk[2 * kTraceWaves];
 __device__ __forceinline__ unsigned int xcc_id() {
     unsigned int r;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(r));
@@ -1105,6 +1112,7 @@ __device__ __forceinline__ unsigned int xcc_id() {
         if ((threadIdx.x & 63u) == 0 && (w) < kTraceWaves) {                              \
             g_mck_trace[3 * (w) + (k)] = wall_clock64();                                  \
             if ((k) == 0) g_mck_trace_xcc[(w)] = xcc_id();                                \
+            if ((k) != 1) g_mck_trace_clk[2 * (w) + ((k) >> 1)] = clock64();              \
         }                                                                                 \
     } while (0)
 #else
@@ -1597,11 +1605,11 @@ __device__ __forceinline__ uint64_t tail64(const uint8_t *lds, const crc64_gpu_p
     return x;
 }
 
-// CRC-64 counterpart of payload32_g64.
+// CRC-64 counterpart of payload32_g64 (a non-zero RAW `reg` needs len >= 8).
 template <bool NT, bool RAW = false, int OM = kOpsLds>
 __device__ __forceinline__ uint64_t payload64_g64(const uint8_t *lds, const crc64_gpu_pack_t *pk, const uint8_t *p,
-                                                  uint64_t len, uint32_t gl, uint32_t lc) {
-    const uint64_t init = RAW ? 0ull : pk->init;
+                                                  uint64_t len, uint32_t gl, uint32_t lc, uint64_t reg = 0ull) {
+    const uint64_t init = RAW ? reg : pk->init;
     const uint64_t sa = reinterpret_cast<uint64_t>(p), ea = sa + len;
     const uint64_t a0 = sa & ~15ull, a1 = (ea + kGridAlign - 1) & ~(kGridAlign - 1);
     const uint32_t W = (uint32_t)(a1 - a0);

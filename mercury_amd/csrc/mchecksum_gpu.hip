@@ -695,6 +695,11 @@ MCHECKSUM_PUBLIC int mck_debug_trace_xcc_read(void *host, size_t bytes) {
     if (bytes > sizeof(g_mck_trace_xcc)) bytes = sizeof(g_mck_trace_xcc);
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_mck_trace_xcc), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
+// ... the shader-clock stamps (entry, exit) of each wave of the last launch ...
+MCHECKSUM_PUBLIC int mck_debug_trace_clk_read(void *host, size_t bytes) {
+    if (bytes > sizeof(g_mck_trace_clk)) bytes = sizeof(g_mck_trace_clk);
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_mck_trace_clk), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
 // ... and the work-queue fault records (count, then 4 words per record).
 MCHECKSUM_PUBLIC int mck_debug_qdiag_read(unsigned int *n, unsigned long long *rec) {
     if (hipMemcpyFromSymbol(n, HIP_SYMBOL(g_mck_qdiag_n), sizeof(*n), 0, hipMemcpyDeviceToHost) != hipSuccess) return -1;

@@ -540,22 +540,25 @@ __global__ __launch_bounds__(256) void core_header_kernel(HdrArgs a) {
 // integer in little-endian order, or the raw bytes of an opaque/raw field.
 //
 // One wave per message, the schema walk wave-uniform (the schema rides in the
-// kernel arguments).  The register L of the hashed stream (zero init, no
-// finalisation) is built field by field: an integer updates it byte by byte
-// from an LDS byte table; an opaque or raw field of n bytes is cut into 64
-// lane ranges hashed byte by byte, each shifted past the bytes after it
-// (Z^k from the base-16 digit tables) and XOR-reduced over the wave, then
-// L <- Z^n(L) ^ that.  CRC = L ^ Z^N(init) ^ xorout, N = hashed byte count.
+// kernel arguments).  The register L of the hashed stream starts at the
+// model's initial value and is built field by field: an integer updates it
+// byte by byte from an LDS byte table; an opaque or raw field of n bytes is
+// cut into 64 lane ranges hashed byte by byte, each shifted past the bytes
+// after it (Z^k from the base-16 digit tables) and XOR-reduced over the
+// wave, then L <- Z^n(L) ^ that.  CRC = L ^ xorout.
 //
 // Large batches (the throughput layout, round 3) run the same walk in
 // persistent 1024-thread workgroups that also hold the payload kernels' LDS
 // tables: an opaque or raw field of >= kXdrFastMin bytes is hashed by the
 // payload step loop (coalesced 1 KiB steps, payload32_g64 / payload64_g64 in
 // RAW form: zero init, no finalisation) instead of 64 byte-serial lane
-// ranges, and messages come from the work queue (crc_gpu_device.h) -- an
-// iovec message (hg_perf_proc_iovec, Testing/perf/hg/mercury_perf.c:897-923:
-// a u32 length, then the bytes) then costs about what the same payload costs
-// through the offsets kernel.
+// ranges, and messages come from the work queue (crc_gpu_device.h).  The
+// step loop starts from the running register itself (it rides in the field's
+// first bytes, R(L, M) = R(0, M ^ L)), so such a field needs no Z^n shift:
+// an iovec message (hg_perf_proc_iovec, Testing/perf/hg/mercury_perf.c:897-923:
+// a u32 length, then the bytes) costs its 4-byte table walk plus what the
+// same payload costs through the offsets kernel -- no dependent chain of
+// digit-table loads per message (round 3: two Z^n shifts per message before).
 constexpr uint32_t kXdrMaxFields = 64;
 constexpr uint64_t kXdrFastMin = 256;
 
@@ -593,17 +596,17 @@ __device__ __forceinline__ xdr_reg_t<W> xdr_tab_entry(uint64_t rpoly, uint32_t t
 }
 
 // One message (one wave, wave-uniform walk): writes out[m] and status[m].
-// fast(p, len, &L) may hash an opaque/raw field of len bytes at p itself
-// (returning true with L = its linear CRC); otherwise 64 lane ranges are
-// hashed byte by byte.
+// fast(p, len, &L) may hash an opaque/raw field of len bytes at p itself,
+// continuing the running register L (returning true); otherwise 64 lane
+// ranges are hashed byte by byte and combined into L.
 template <int W, class Fast>
 __device__ __forceinline__ void xdr_message(const XdrArgs &a, uint64_t m, const xdr_reg_t<W> *tab, uint32_t lane,
                                             Fast &&fast) {
     using R = xdr_reg_t<W>;
     uint64_t pos = a.off[m];
     const uint64_t end = a.off[m + 1];
-    R acc = 0;
-    uint64_t N = 0, last = 0;
+    R acc = (R)a.init;
+    uint64_t last = 0;
     bool bad = end < pos;
     for (uint32_t f = 0; f < a.nf && !bad; f++) {
         const uint32_t kind = a.kind[f], sz = a.size[f];
@@ -621,7 +624,6 @@ __device__ __forceinline__ void xdr_message(const XdrArgs &a, uint64_t m, const 
             for (uint32_t b = 0; b < slot; b++) v = v << 8 | a.buf[pos + b];
             for (uint32_t b = 0; b < sz; b++) acc = (acc >> 8) ^ tab[(uint32_t)(acc ^ (R)(v >> (8 * b))) & 0xFFu];
             last = sz == 8 ? v : v & ((1ull << (8 * sz)) - 1);
-            N += sz;
             pos += slot;
             continue;
         }
@@ -631,21 +633,20 @@ __device__ __forceinline__ void xdr_message(const XdrArgs &a, uint64_t m, const 
             bad = true;
             break;
         }
-        R p = 0;
-        if (!fast(a.buf + pos, len, &p)) {
+        if (!fast(a.buf + pos, len, &acc)) {
+            R p = 0;
             const uint64_t chunk = (len + 63) / 64;
             const uint64_t lo = lane * chunk < len ? lane * chunk : len, hi = lo + chunk < len ? lo + chunk : len;
             for (uint64_t i = lo; i < hi; i++) p = (p >> 8) ^ tab[(uint32_t)(p ^ a.buf[pos + i]) & 0xFFu];
             p = xdr_shift<W>(a.shift, p, len - hi);
 #pragma unroll
             for (int k = 1; k < 64; k <<= 1) p ^= __shfl_xor(p, k, 64);
+            acc = xdr_shift<W>(a.shift, acc, len) ^ p;
         }
-        acc = xdr_shift<W>(a.shift, acc, len) ^ p;
-        N += len;
         pos += raw ? len : (len + 3) & ~3ull;
     }
     if (lane == 0) {
-        const R crc = bad ? (R)0 : acc ^ xdr_shift<W>(a.shift, (R)a.init, N) ^ (R)a.xorout;
+        const R crc = bad ? (R)0 : acc ^ (R)a.xorout;
         reinterpret_cast<R *>(a.out)[m] = crc;
         if (a.status) a.status[m] = bad ? 1 : 0;
     }
@@ -686,14 +687,14 @@ __global__ __launch_bounds__(1024, 1) void xdr_fast_kernel(XdrArgs a) {
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 16u + (threadIdx.x >> 6));
     const uint32_t nw = gridDim.x * 16u;
     const uint32_t lc0 = (lane & 31u) << 2, lc1 = lc0 | 0x10000u, lc64 = (lane & 31u) << 3;
-    auto fast = [&](const uint8_t *p, uint64_t len, R *out) -> bool {
+    auto fast = [&](const uint8_t *p, uint64_t len, R *reg) -> bool {
         if (len < kXdrFastMin || len >= (1ull << 31)) return false;
         if constexpr (W == 32)
-            *out = payload32_g64<NT, Tab32<false>, true>(Tab32<false>{lds}, reinterpret_cast<const crc32_gpu_pack_t *>(a.pack),
-                                                         p, len, lane, lc0, lc1);
+            *reg = payload32_g64<NT, Tab32<false>, true>(Tab32<false>{lds}, reinterpret_cast<const crc32_gpu_pack_t *>(a.pack),
+                                                         p, len, lane, lc0, lc1, *reg);
         else
-            *out = payload64_g64<NT, true, kOpsGlobal>(lds, reinterpret_cast<const crc64_gpu_pack_t *>(a.pack), p, len,
-                                                       lane, lc64);
+            *reg = payload64_g64<NT, true, kOpsGlobal>(lds, reinterpret_cast<const crc64_gpu_pack_t *>(a.pack), p, len,
+                                                       lane, lc64, *reg);
         return true;
     };
     const bool faulted = for_each_unit<true>(&wgq, a.queue, a.count, wave, nw,

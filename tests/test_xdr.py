@@ -106,7 +106,9 @@ def test_gpu_xdr_test_proc_fixtures(gpu, method, layout, monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("layout", LAYOUTS)
-@pytest.mark.parametrize("method", ["crc32c", "crc64"])
+# crc64-jones: zero initial value (the running register the step loop starts
+# from is then 0 at the first field); crc32: a second 32-bit polynomial
+@pytest.mark.parametrize("method", ["crc32c", "crc64", "crc64-jones", "crc32"])
 @pytest.mark.parametrize("kind", ["iovec", "mixed"])
 def test_gpu_xdr_random_messages(gpu, oracle_mod, method, kind, layout, monkeypatch):
     monkeypatch.setenv("MCHECKSUM_GPU_XDR_FAST", layout)

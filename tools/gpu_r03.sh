@@ -6,6 +6,7 @@
 #             env pseudo-variants in AB_ENV, on AB_CONFIGS
 #   bench  -- bench.py per CONFIGS into gpurun_out/r03/bench_<config>.json
 #   trace  -- rocprofv3 kernel-trace summaries of bench.py per CONFIGS
+#   xcd    -- per-XCD end time and shader clock (tools/xcd_clock.py, trace build)
 #   pmc    -- FETCH_SIZE / WRITE_SIZE passes per CONFIGS -> pmc_traffic_<config>.json
 # Every GPU step has its own time limit; the first failure ends the script.
 set -o pipefail
@@ -51,6 +52,11 @@ if [ "$P" = driver ]; then
   step "bench driver-style"
   timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_driver.json 2> $O/bench_driver.err || { tail -20 $O/bench_driver.err; exit 1; }
   cat $O/bench_driver.json
+fi
+if [ "$P" = xcd ]; then
+  step "xcd clock ${XCD_CONFIGS:-c2}"
+  timeout -k 10 300 python tools/xcd_clock.py ${XCD_CONFIGS:-c2} --out $O/xcd_clock.json > $O/xcd_clock.log 2>&1; rc=$?
+  grep -v amdgpu.ids $O/xcd_clock.log | tail -25; [ $rc -eq 0 ] || exit $rc
 fi
 if [ "$P" = trace ]; then
   cd /tmp && export TMPDIR=/tmp
