@@ -201,17 +201,25 @@ constexpr uint64_t kSplitBytes = 256u << 10;
 // chunk id, so fetches run in chunk order and the first "no more chunks" is
 // final -- and the fetch's latency hides under the rest of the chunk.  Chunk
 // ids pass through a small LDS ring whose entries are recycled only after all
-// readers of the previous occupant have read it.  Exit counting is
-// hierarchical (LDS per workgroup, one line per group, one per slot) and the
-// last group zeroes the slot for the next launch (the host hands each launch
-// a slot of its stream's own, mchecksum_gpu.hip).  tests/test_queue_model.py
+// readers of the previous occupant have read it (the host hands each launch a
+// slot of its stream's own, mchecksum_gpu.hip).  tests/test_queue_model.py
 // runs the same protocol on the CPU under random interleavings.
-// Slot layout (one counter per 256-B line): [0, 8) sub-queue tickets,
-// [8, 16) exited workgroups per group (blockIdx % 8), [16] exited groups,
-// [17] fault flag of the launch -- all zeroed by the launch's last group --
-// and [18] the number of launches completed on the slot (never zeroed: the
-// host compares it with the launches it issued before it gives the slot to
-// another stream, mchecksum_gpu.hip queue_slot).
+//
+// Two banks per slot (round 3).  Launch s on a slot counts in bank s & 1 (the
+// host passes that bank) and, from its first workgroup at entry, zeroes the
+// protocol lines of the OTHER bank, which the slot's next launch will use --
+// launches on a slot never overlap, so nobody is using that bank.  Round 2
+// instead had the launch's last group zero its own bank at exit, behind a
+// hierarchical exit count (LDS per workgroup, a line per group, one per
+// slot): three dependent device-scope atomics, the zeroing and a wait after
+// the last wave's last payload, on every launch's critical path.  Now a
+// workgroup's exit is one non-returning add on its group's completion line.
+// Bank layout (one counter per 256-B line, 8 KiB per bank, 16 KiB-aligned
+// slots): [0, 8) sub-queue tickets, [8] fault flag of the launch -- both
+// zeroed by the previous launch on the slot -- and [9, 17) completed
+// workgroups per group (blockIdx % 8; never zeroed: the host sums both
+// banks' and compares with the workgroups it issued before it gives the slot
+// to another stream, queue_slot).
 //
 // Exclusivity.  A slot serves one launch at a time: the host hands the queue
 // only to eager launches, each on a slot of its stream's own (launches on one
@@ -227,12 +235,13 @@ constexpr uint64_t kSplitBytes = 256u << 10;
 // the units such mixed launches hashed twice.)
 constexpr uint32_t kQSub = 8;
 constexpr uint32_t kQStride = 32;  // u64 words between counters
-constexpr uint32_t kQGroupDone = kQSub;
-constexpr uint32_t kQAllDone = 2 * kQSub;
-constexpr uint32_t kQFault = 2 * kQSub + 1;
-constexpr uint32_t kQSlotLines = 2 * kQSub + 2;  // lines a launch leaves zeroed
-constexpr uint32_t kQDone = kQSlotLines;
-constexpr uint32_t kQSlotWords = (kQSlotLines + 1) * kQStride;
+constexpr uint32_t kQFault = kQSub;
+constexpr uint32_t kQBankLines = kQSub + 1;  // protocol lines, zeroed before the bank's next use
+constexpr uint32_t kQDone = kQBankLines;     // [kQDone, kQDone + kQSub): completed workgroups per group
+constexpr uint64_t kQBankBytes = 8192;
+constexpr uint32_t kQBankWords = (uint32_t)(kQBankBytes / 8);
+constexpr uint32_t kQSlotWords = 2 * kQBankWords;  // slots 2 * kQBankBytes aligned: bank ^ kQBankBytes = the other
+static_assert((kQDone + kQSub) * kQStride <= kQBankWords, "bank overflow");
 // Chunk size: a power of two, about a quarter of a workgroup's fair share
 // of units, between 1 and 32 (C4: 32 units; a 5000-payload batch: 4).
 // Fixed 16 starved half the workgroups of C3's 8192 units at 2 WGs per CU; 32
@@ -397,8 +406,11 @@ __device__ bool wg_publish(WgQueue *L, uint32_t seq, uint64_t id, uint32_t cl) {
 }
 
 // Thread 0, before the kernel's first barrier: reset the LDS state and
-// publish the first chunk (its fetch overlaps the LDS table fill).  Without a
-// slot (see "Exclusivity") the workgroup takes the static split (busy = 1).
+// publish the first chunk (its fetch overlaps the LDS table fill); workgroup
+// 0 first zeroes the other bank's protocol lines for the slot's next launch
+// (the fetch's returning atomic waits for those adds to be performed: vmcnt
+// also counts non-returning atomics on gfx9-family parts).  Without a slot
+// (see "Exclusivity") the workgroup takes the static split (busy = 1).
 __device__ __attribute__((unused)) void wg_queue_init(WgQueue *L, unsigned long long *q, uint64_t n) {
     L->slot = 0;
     L->drained = 0;
@@ -409,6 +421,11 @@ __device__ __attribute__((unused)) void wg_queue_init(WgQueue *L, unsigned long 
         L->entry[r] = ~0ull;
     }
     if (!q) return;
+    if (blockIdx.x == 0) {
+        unsigned long long *o = reinterpret_cast<unsigned long long *>(reinterpret_cast<uintptr_t>(q) ^ kQBankBytes);
+#pragma unroll
+        for (uint32_t j = 0; j < kQBankLines; j++) atomicExch(o + j * kQStride, 0ull);
+    }
     const ChunkPlan plan(n);
     (void)wg_publish(L, 0, wg_fetch(L, q, plan.nch), plan.cl);
 }
@@ -423,46 +440,17 @@ __device__ __forceinline__ T wave_max(T v) {
     return v;
 }
 
-// Exit counting of a launch that holds a slot, run by every wave once it has
-// no more units (wave-uniform).  One global atomic per wave on a single line
-// serialised ~4096 x 45 ns at the end of every launch (C2 ran 2x slower), so
-// it is hierarchical: waves count in LDS (*wg_exited), the last wave of a
-// workgroup runs wg_last() and counts in its group's line, the last workgroup
-// of a group in the slot's line; the last group zeroes the slot's protocol
-// lines for the next launch and then, after a fence, counts the launch done.
-#ifndef MCK_SLOT_FENCE
-#define MCK_SLOT_FENCE 0
-#endif
-template <class F>
-__device__ __forceinline__ void slot_exit(unsigned long long *queue, uint32_t *wg_exited, F &&wg_last) {
+// Exit of a launch that holds a slot, run by every wave once it has no more
+// units (wave-uniform): waves count in LDS (*wg_exited); the last wave of a
+// workgroup adds one, without waiting for the result, to its group's
+// completion line of the launch's bank (one add per workgroup, spread over 8
+// lines: one global add per wave on a single line serialised ~4096 x 45 ns
+// and ran C2 2x slower, round 1).
+__device__ __forceinline__ void slot_exit(unsigned long long *queue, uint32_t *wg_exited) {
     const bool l0 = (threadIdx.x & 63u) == 0;
     uint32_t wl = 0;
     if (l0) wl = atomicAdd(wg_exited, 1u) == blockDim.x / 64u - 1u;
-    uint32_t last = 0;
-    if (__builtin_amdgcn_readfirstlane(wl)) {
-        wg_last();
-        if (l0) {
-            const uint32_t g = blockIdx.x % kQSub;
-            const uint32_t wgs = (gridDim.x - g + kQSub - 1) / kQSub;  // workgroups in group g
-            const uint32_t groups = gridDim.x < kQSub ? gridDim.x : kQSub;
-            last = atomicAdd(queue + (kQGroupDone + g) * kQStride, 1ull) == wgs - 1ull &&
-                   atomicAdd(queue + kQAllDone * kQStride, 1ull) == groups - 1ull;
-        }
-    }
-    if (__builtin_amdgcn_readfirstlane(last)) {  // one instruction: lane j zeroes line j
-        const uint32_t j = threadIdx.x & 63u;
-        if (j < kQSlotLines) atomicExch(queue + j * kQStride, 0ull);
-        // The done count must not land before the zeroing: wait until this
-        // wave's atomics have been performed (vmcnt also counts stores and
-        // non-returning atomics on gfx9-family parts).  An agent-scope fence
-        // would also write back the whole L2 (buffer_wbl2).
-#if MCK_SLOT_FENCE
-        __threadfence();
-#else
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
-        if (j == 0) atomicAdd(queue + kQDone * kQStride, 1ull);
-    }
+    if (l0 && wl) atomicAdd(queue + (kQDone + blockIdx.x % kQSub) * kQStride, 1ull);
 }
 
 // Calls body(u) for this wave's units: through the work queue (DYN: the
@@ -592,11 +580,11 @@ __device__ __forceinline__ bool for_each_unit(WgQueue *L, unsigned long long *qu
         }
 #endif
         if (__builtin_amdgcn_readfirstlane(lds_ld(&L->busy))) return false;  // no slot
-        // The first faulting wave of the launch claims the slot's fault flag
+        // The first faulting wave of the launch claims the bank's fault flag
         // (before its own exit is counted, so the slot cannot be released yet).
         uint32_t first = 0;
         if (l0 && flt) first = atomicCAS(queue + kQFault * kQStride, 0ull, 1ull) == 0ull;
-        slot_exit(queue, &L->exited, [] {});
+        slot_exit(queue, &L->exited);
         (void)nw;
         return __builtin_amdgcn_readfirstlane(first) != 0;
     } else {

@@ -24,7 +24,8 @@ constexpr uint32_t kQueueSlots = kStreamSlots;
 // owned by one stream at a time.
 struct SlotState {
     uintptr_t sid = 0;  // owning stream (handle)
-    uint64_t issued = 0;         // launches handed this slot (the kernels count completions, kQDone)
+    uint64_t issued = 0;         // launches handed this slot: launch s counts in bank s & 1
+    uint64_t issued_wgs = 0;     // their workgroups (each counts its completion, kQDone)
     uint64_t last_use = 0;       // LRU tick
     bool owned = false;
 };
@@ -35,28 +36,31 @@ struct DevCtx {
     void *pack[MCK_NMODELS][CRC_GPU_MAX_LOG2G + 1] = {};
     void *ext[MCK_NMODELS] = {};  // mchecksum_gpu_ext.hip's per-model tables
     // Work-queue slots of the batch kernels (WgQueue, crc_gpu_device.h):
-    // kQueueSlots zeroed counter sets; a launch's last group re-zeroes its slot.
+    // kQueueSlots zeroed counter sets of two banks each (crc_gpu_device.h):
+    // launch s on a slot uses bank s & 1 and zeroes the other for launch s + 1.
     // Eager launches use a slot of their stream's own (keyed by the handle);
     // launches on one stream never overlap.  When all slots are owned, the
-    // least recently used slot whose issued launches have all completed
+    // least recently used slot whose issued workgroups have all completed
     // (kQDone) changes owner.
     // Graph-captured launches, and streams that find no idle slot, get none
     // and take the plain static split (crc_gpu_device.h, "Exclusivity").
-    unsigned long long *queue = nullptr;
+    unsigned long long *queue = nullptr;        // 2 * kQBankBytes-aligned view of queue_mem
+    void *queue_mem = nullptr;
     SlotState slot[kQueueSlots];               // guarded by g_mu
     std::unordered_map<uintptr_t, uint32_t> sid_slot;  // guarded by g_mu
     uint32_t nslots = 0;                        // slots handed out so far
     uint64_t tick = 0;
     hipStream_t probe = nullptr;                // private stream: reads kQDone words
-    unsigned long long *probe_host = nullptr;   // pinned word for those reads
+    unsigned long long *probe_host = nullptr;   // pinned copy of one slot for those reads
     // diagnostics (mchecksum_gpu_queue_stats)
     long long n_slot = 0, n_noslot = 0, n_reclaim = 0, n_busy_skip = 0;
 };
 
-// A launch's slot (counters) and its index.
+// A launch's slot bank (counters), the slot's index and the launch's grid.
 struct SlotRef {
     unsigned long long *q = nullptr;
     int idx = -1;
+    uint32_t grid = 0;
 };
 
 extern std::mutex g_mu;
@@ -80,12 +84,13 @@ int prologue(const char *method, int log2g, int *width, DevCtx **c, const void *
 // Z^n shift pack of a 32/64-bit model, the byte table of a 16-bit one
 // (caller holds g_mu).
 int get_ext(DevCtx *c, int idx, const void **out);
-// Work-queue slot for one launch of a throughput (non-light) batch kernel on
-// `stream`, exclusive to that stream; empty (static split) for a launch being
-// captured into a graph or a stream that finds no idle slot.  Every launch
-// given a slot must count itself done on it (slot_exit): if the launch fails
-// to start, slot_unissue() takes the launch back.
-SlotRef queue_slot(DevCtx *c, void *stream);
+// Work-queue slot bank for one launch of `grid` workgroups of a throughput
+// (non-light) batch kernel on `stream`, exclusive to that stream; empty
+// (static split) for a launch being captured into a graph or a stream that
+// finds no idle slot.  Every workgroup of a launch given a slot must count
+// itself done on it (slot_exit): if the launch fails to start,
+// slot_unissue() takes the launch back.
+SlotRef queue_slot(DevCtx *c, void *stream, uint32_t grid);
 void slot_unissue(DevCtx *c, const SlotRef &r);
 // Queue-fault count of mchecksum_gpu_ext.hip's kernels (their own copy of
 // g_mck_queue_faults) on the current device; -1 on error.

@@ -127,14 +127,20 @@ int device_ctx(DevCtx **out) {
         e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         if (e != hipSuccess) return hip_err(e, "hipDeviceGetAttribute");
         c.cus = cus > 0 ? cus : 1;
-        const size_t qbytes = (size_t)kQueueSlots * kQSlotWords * sizeof(unsigned long long);
-        e = hipMalloc(reinterpret_cast<void **>(&c.queue), qbytes);
-        if (e == hipSuccess) e = hipMemset(c.queue, 0, qbytes);
+        // slots aligned to two banks, so a bank's partner is its address ^ kQBankBytes
+        const size_t slot_bytes = (size_t)kQSlotWords * sizeof(unsigned long long);
+        const size_t qbytes = (size_t)kQueueSlots * slot_bytes + slot_bytes;
+        e = hipMalloc(&c.queue_mem, qbytes);
+        if (e == hipSuccess) e = hipMemset(c.queue_mem, 0, qbytes);
+        if (e == hipSuccess)
+            c.queue = reinterpret_cast<unsigned long long *>((reinterpret_cast<uintptr_t>(c.queue_mem) + slot_bytes - 1) /
+                                                             slot_bytes * slot_bytes);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&c.probe, hipStreamNonBlocking);
-        if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&c.probe_host), sizeof(unsigned long long));
+        if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&c.probe_host), slot_bytes);
         if (e != hipSuccess) {
-            if (c.queue) (void)hipFree(c.queue);
+            if (c.queue_mem) (void)hipFree(c.queue_mem);
             if (c.probe) (void)hipStreamDestroy(c.probe);
+            c.queue_mem = nullptr;
             c.queue = nullptr;
             c.probe = nullptr;
             return hip_err(e, "work-queue allocation");
@@ -182,20 +188,23 @@ int get_pack(DevCtx *c, int idx, int log2g, const void **pack) {
     return 0;
 }
 
-// Whether slot i has completed every launch it was issued (its kernels'
-// kQDone counter, read on the private stream); false if the read fails
+// Whether slot i has completed every workgroup it was issued (the kQDone
+// lines of both banks, read on the private stream); false if the read fails
 // (caller holds g_mu).
 bool slot_idle(DevCtx *c, uint32_t i) {
-    if (hipMemcpyAsync(c->probe_host, c->queue + (size_t)i * kQSlotWords + kQDone * kQStride,
-                       sizeof(unsigned long long), hipMemcpyDeviceToHost, c->probe) != hipSuccess ||
+    if (hipMemcpyAsync(c->probe_host, c->queue + (size_t)i * kQSlotWords, (size_t)kQSlotWords * sizeof(unsigned long long),
+                       hipMemcpyDeviceToHost, c->probe) != hipSuccess ||
         hipStreamSynchronize(c->probe) != hipSuccess) {
         (void)hipGetLastError();
         return false;
     }
-    return *c->probe_host == c->slot[i].issued;
+    uint64_t done = 0;
+    for (uint32_t b = 0; b < 2; b++)
+        for (uint32_t g = 0; g < kQSub; g++) done += c->probe_host[b * kQBankWords + (kQDone + g) * kQStride];
+    return done == c->slot[i].issued_wgs;
 }
 
-SlotRef queue_slot(DevCtx *c, void *stream) {
+SlotRef queue_slot(DevCtx *c, void *stream, uint32_t grid) {
     SlotRef r;
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing((hipStream_t)stream, &st) != hipSuccess) {
@@ -269,11 +278,13 @@ SlotRef queue_slot(DevCtx *c, void *stream) {
         s.sid = sid;
         c->sid_slot[sid] = i;
     }
+    r.q = c->queue + (size_t)i * kQSlotWords + (s.issued & 1u) * kQBankWords;
+    r.idx = (int)i;
+    r.grid = grid;
     s.issued++;
+    s.issued_wgs += grid;
     s.last_use = ++c->tick;
     c->n_slot++;
-    r.q = c->queue + (size_t)i * kQSlotWords;
-    r.idx = (int)i;
     return r;
 }
 
@@ -281,6 +292,7 @@ void slot_unissue(DevCtx *c, const SlotRef &r) {
     if (r.idx < 0) return;
     std::lock_guard<std::mutex> lk(g_mu);
     c->slot[r.idx].issued--;
+    c->slot[r.idx].issued_wgs -= r.grid;
 }
 
 uint32_t *error_word() { return t_err_word; }
@@ -448,9 +460,10 @@ int do_offsets(const char *method, const void *base, const uint64_t *offsets, si
         k = verify ? (nt ? kernel_ptr<64, 6, kOffsets, true, true>() : kernel_ptr<64, 6, kOffsets, true>())
                    : (nt ? kernel_ptr<64, 6, kOffsets, false, true>() : kernel_ptr<64, 6, kOffsets, false>());
     SlotRef sr;
-    if (dyn_policy(width, kOffsets, nt, light)) sr = queue_slot(c, stream);
+    const unsigned grid = grid_for(c, count, k);
+    if (dyn_policy(width, kOffsets, nt, light)) sr = queue_slot(c, stream, grid);
     a.queue = sr.q;
-    rc = launch(k, a, grid_for(c, count, k), stream);
+    rc = launch(k, a, grid, stream);
     if (rc != MCHECKSUM_GPU_OK) slot_unissue(c, sr);
     if (rc == MCHECKSUM_GPU_OK && gpu_msb(midx) && !verify) rc = swap_outputs(out, count, width, stream);
     return rc;
@@ -513,9 +526,10 @@ int launch_fixed(DevCtx *c, int idx, const void *pack, int width, int lg, const 
                                        Shape<64, kFixedAligned>::blocks_per_cu}
                              : KLaunch{crc64_batch_kernel<6, kFixedAligned, false, false, true>, Shape<64, kFixedAligned>::block,
                                        Shape<64, kFixedAligned>::blocks_per_cu};
-        const SlotRef sr = queue_slot(c, stream);
+        const unsigned grid = grid_for(c, (uint64_t)count << sl, k);
+        const SlotRef sr = queue_slot(c, stream, grid);
         a.queue = sr.q;
-        int rc = launch(k, a, grid_for(c, (uint64_t)count << sl, k), stream);
+        int rc = launch(k, a, grid, stream);
         if (rc != MCHECKSUM_GPU_OK) slot_unissue(c, sr);
         if (rc == MCHECKSUM_GPU_OK && gpu_msb(idx)) rc = swap_outputs(dev_out, count, width, stream);
         return rc;
@@ -532,7 +546,7 @@ int launch_fixed(DevCtx *c, int idx, const void *pack, int width, int lg, const 
         blocks = (unsigned)(units < (uint64_t)c->cus ? (units ? units : 1) : c->cus);
     SlotRef sr;
     if (dyn) {
-        sr = queue_slot(c, stream);
+        sr = queue_slot(c, stream, blocks);
         a.queue = sr.q;
     }
     int rc = launch(k, a, blocks, stream);

@@ -1,8 +1,10 @@
 """CPU model of the batch kernels' work-queue protocol (crc_gpu_device.h:
 WgQueue, wg_fetch, wg_publish, for_each_unit), run under random interleavings
 of every wave's shared-memory steps.  Checks what the GPU relies on: every
-unit is processed exactly once, no wait can block forever, and the last
-workgroup leaves the slot's counters at zero for the next launch.
+unit is processed exactly once, no wait can block forever, and every launch
+leaves the bank the slot's next launch counts in at zero (two banks per slot,
+round 3: launch s counts in bank s & 1 and its first workgroup zeroes the
+other), with one completion per workgroup counted.
 
 Each wave is a generator that yields at every access to shared state (LDS or
 the global slot), so a seeded scheduler explores many orders of the same
@@ -11,7 +13,7 @@ per-thread stream, streams past the table: crc_gpu_device.h "Exclusivity")
 takes the static split and never touches any slot; the fail-closed fault flag
 is modelled too.  Fetch triggers, chunk sizes (chunk_log2, the
 quarter-size tail chunks of ChunkPlan), the
-round-robin sub-queues, the LDS ring recycling and the hierarchical exit
+round-robin sub-queues, the LDS ring recycling, the bank zeroing and the exit
 counting mirror the device code one to one.
 """
 import random
@@ -29,15 +31,33 @@ def chunk_log2(n, grid, max_log2=5):
     return lg
 
 
-class Slot:
+class Bank:
     def __init__(self):
         self.sub = [0] * QSUB          # sub-queue tickets
-        self.group_done = [0] * QSUB   # exited workgroups per group
-        self.all_done = 0
         self.fault = 0                 # first faulting wave of the launch
+        self.done = [0] * QSUB         # completed workgroups per group (never zeroed)
+
+    def zero(self):  # wg_queue_init, workgroup 0: the protocol lines only
+        self.sub = [0] * QSUB
+        self.fault = 0
 
     def clean(self):
-        return self.sub == [0] * QSUB and self.group_done == [0] * QSUB and self.all_done == 0 and self.fault == 0
+        return self.sub == [0] * QSUB and self.fault == 0
+
+
+class Slot:
+    def __init__(self):
+        self.banks = [Bank(), Bank()]
+        self.issued = 0       # launches handed this slot (host: SlotState::issued)
+        self.issued_wgs = 0   # their workgroups (host: SlotState::issued_wgs)
+
+    def completed_wgs(self):
+        return sum(sum(b.done) for b in self.banks)
+
+    def clean(self):
+        """Ready for the next launch: the bank it will count in is zeroed and
+        every workgroup issued so far has counted itself done."""
+        return self.banks[self.issued & 1].clean() and self.completed_wgs() == self.issued_wgs
 
 
 class Lds:
@@ -70,7 +90,12 @@ def run_launches(launches, seed, slot=None, max_steps=4_000_000):
     for spec in launches:
         r = dict(units=[], slot=slot, faulted_waves=0, first_faults=0, busy_wgs=0)
         results.append(r)
-        gens += _launch(spec, slot, rnd, r)
+        bank = None
+        if not spec.get("no_slot"):  # queue_slot: bank issued & 1, then count the launch
+            bank = (slot.banks[slot.issued & 1], slot.banks[(slot.issued & 1) ^ 1])
+            slot.issued += 1
+            slot.issued_wgs += spec["grid"]
+        gens += _launch(spec, bank, rnd, r)
     steps = 0
     while gens:
         g = rnd.choice(gens)
@@ -85,7 +110,7 @@ def run_launches(launches, seed, slot=None, max_steps=4_000_000):
     return results
 
 
-def _launch(spec, slot, rnd, res):
+def _launch(spec, bank, rnd, res):
     n, grid, waves_per_wg, drop = spec["n"], spec["grid"], spec["wpw"], spec.get("drop")
     cl = chunk_log2(n, grid)
     cu, lead = 1 << cl, max(1, (1 << cl) // 4) if (1 << cl) > 4 else 1
@@ -104,14 +129,15 @@ def _launch(spec, slot, rnd, res):
         return 1 << cl if cid < nbig else 1 << sl
     done_units = res["units"]
     lds = [Lds() for _ in range(grid)]
+    cur, other = bank if bank else (None, None)
 
     def fetch(L, b):  # wg_fetch
         home = b % QSUB
         d = L.drained
         while d < QSUB:
             k = (home + d) % QSUB
-            t = slot.sub[k]
-            slot.sub[k] += 1
+            t = cur.sub[k]
+            cur.sub[k] += 1
             yield
             if k + t * QSUB < nch:
                 return k + t * QSUB
@@ -169,31 +195,17 @@ def _launch(spec, slot, rnd, res):
                     yield
         if flt:
             res["faulted_waves"] += 1
-            first = slot.fault == 0  # atomicCAS(fault, 0, 1)
-            slot.fault = 1
+            first = cur.fault == 0  # atomicCAS(fault, 0, 1)
+            cur.fault = 1
             yield
             res["first_faults"] += first
-        # hierarchical exit counting
+        # slot_exit: the workgroup's last wave counts it done on its group's line
         prev_ex = L.exited  # atomicAdd on LDS: the returned old value decides
         L.exited += 1
         yield
         if prev_ex == waves_per_wg - 1:
-            g = b % QSUB
-            wgs = (grid - g + QSUB - 1) // QSUB
-            groups = min(grid, QSUB)
-            prev = slot.group_done[g]
-            slot.group_done[g] += 1
+            cur.done[b % QSUB] += 1
             yield
-            if prev == wgs - 1:
-                prev_all = slot.all_done
-                slot.all_done += 1
-                yield
-                if prev_all == groups - 1:
-                    slot.sub = [0] * QSUB
-                    slot.group_done = [0] * QSUB
-                    slot.all_done = 0
-                    slot.fault = 0
-                    yield
 
     def init(b):  # wg_queue_init (thread 0 of the workgroup, before the barrier)
         L = lds[b]
@@ -201,6 +213,9 @@ def _launch(spec, slot, rnd, res):
         if L.busy:
             res["busy_wgs"] += 1
         else:
+            if b == 0:
+                other.zero()  # the slot's next launch counts there
+                yield
             yield from publish(L, 0, (yield from fetch(L, b)))
         yield
         L.ready = True
@@ -257,3 +272,17 @@ def test_injected_give_up_is_reported_once(n, grid, drop):
     missing = set(range(n)) - set(r["units"])
     assert len(missing) == 1 and len(r["units"]) == n - 1
     assert r["slot"].clean()
+
+
+def test_fault_flag_is_cleared_before_its_bank_is_reused():
+    """A launch that faults leaves its bank's fault flag set; the slot's next
+    launch (other bank) zeroes it, so the launch after that -- back on the
+    faulted bank -- starts clean and claims no fault it did not have."""
+    slot = Slot()
+    r = run_launches([dict(n=900, grid=4, wpw=4, drop=(2, 1))], 11, slot)[0]
+    assert r["first_faults"] == 1 and slot.banks[0].fault == 1
+    for seed in (12, 13, 14):
+        r = run_launches([dict(n=900, grid=4, wpw=4)], seed, slot)[0]
+        assert r["units"] == list(range(900)) and r["first_faults"] == 0
+        assert slot.clean()
+    assert slot.banks[0].fault == 0 and slot.completed_wgs() == 16
