@@ -28,7 +28,8 @@
  * asynchronous and capture-safe once mchecksum_gpu_prepare() has run for the
  * method on the current device (it uploads the lookup tables).  Large batches
  * balance their payloads through a device-side work-queue slot of their
- * stream's own (launches on one stream never overlap).
+ * stream's own (launches on one stream never overlap; host threads may share
+ * a stream -- each launch takes the slot's launch lock while it is enqueued).
  * (A handle names a new stream only after hipStreamDestroy of the old one,
  * which returns once that stream's work has completed, so a reused handle
  * never shares its slot with launches in flight.)  A device has 2048 slots; once all are owned,

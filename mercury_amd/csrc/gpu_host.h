@@ -24,8 +24,8 @@ constexpr uint32_t kQueueSlots = kStreamSlots;
 // owned by one stream at a time.
 struct SlotState {
     uintptr_t sid = 0;  // owning stream (handle)
-    uint64_t issued = 0;         // launches handed this slot: launch s counts in bank s & 1
-    uint64_t issued_wgs = 0;     // their workgroups (each counts its completion, kQDone)
+    uint64_t issued_wgs = 0;     // workgroups of the launches handed this slot (each counts its completion, kQDone)
+    uint64_t seq = 0;            // launches enqueued on the slot: launch s counts in bank s & 1 (guarded by its launch lock)
     uint64_t last_use = 0;       // LRU tick
     bool owned = false;
 };
@@ -52,15 +52,23 @@ struct DevCtx {
     uint64_t tick = 0;
     hipStream_t probe = nullptr;                // private stream: reads kQDone words
     unsigned long long *probe_host = nullptr;   // pinned copy of one slot for those reads
+    // Launch locks (slot i: launch_mu[i % kLaunchLocks]), held from the bank
+    // choice through the kernel's enqueue: two host threads launching on one
+    // stream then enqueue in bank order, so the device alternates the banks.
+    static constexpr uint32_t kLaunchLocks = 64;
+    std::mutex launch_mu[kLaunchLocks];
     // diagnostics (mchecksum_gpu_queue_stats)
     long long n_slot = 0, n_noslot = 0, n_reclaim = 0, n_busy_skip = 0;
 };
 
-// A launch's slot bank (counters), the slot's index and the launch's grid.
+// A launch's slot bank (counters), the slot's index and the launch's grid;
+// holds the slot's launch lock until the launch is enqueued (end of scope)
+// or taken back (slot_unissue).
 struct SlotRef {
     unsigned long long *q = nullptr;
     int idx = -1;
     uint32_t grid = 0;
+    std::unique_lock<std::mutex> lk;
 };
 
 extern std::mutex g_mu;
@@ -89,9 +97,10 @@ int get_ext(DevCtx *c, int idx, const void **out);
 // (static split) for a launch being captured into a graph or a stream that
 // finds no idle slot.  Every workgroup of a launch given a slot must count
 // itself done on it (slot_exit): if the launch fails to start,
-// slot_unissue() takes the launch back.
+// slot_unissue() takes the launch back.  Keep the SlotRef alive until the
+// kernel is enqueued: it holds the slot's launch lock.
 SlotRef queue_slot(DevCtx *c, void *stream, uint32_t grid);
-void slot_unissue(DevCtx *c, const SlotRef &r);
+void slot_unissue(DevCtx *c, SlotRef &r);
 // Queue-fault count of mchecksum_gpu_ext.hip's kernels (their own copy of
 // g_mck_queue_faults) on the current device; -1 on error.
 long long ext_queue_faults();

@@ -221,7 +221,7 @@ SlotRef queue_slot(DevCtx *c, void *stream, uint32_t grid) {
     }
     // hipStreamPerThread names a different stream in every host thread: one
     // slot for that handle could serve two launches at once
-    std::lock_guard<std::mutex> lk(g_mu);
+    std::unique_lock<std::mutex> lk(g_mu);
     if ((hipStream_t)stream == hipStreamPerThread) {
         c->n_noslot++;
         return r;
@@ -278,20 +278,26 @@ SlotRef queue_slot(DevCtx *c, void *stream, uint32_t grid) {
         s.sid = sid;
         c->sid_slot[sid] = i;
     }
-    r.q = c->queue + (size_t)i * kQSlotWords + (s.issued & 1u) * kQBankWords;
-    r.idx = (int)i;
-    r.grid = grid;
-    s.issued++;
-    s.issued_wgs += grid;
+    s.issued_wgs += grid;  // busy from here on: no other stream can reclaim it
     s.last_use = ++c->tick;
     c->n_slot++;
+    lk.unlock();
+    // The bank is chosen under the slot's launch lock, held until the caller
+    // has enqueued the kernel: launches of several host threads on one stream
+    // reach the device in the order of their banks.
+    r.lk = std::unique_lock<std::mutex>(c->launch_mu[i % DevCtx::kLaunchLocks]);
+    r.q = c->queue + (size_t)i * kQSlotWords + (s.seq & 1u) * kQBankWords;
+    s.seq++;
+    r.idx = (int)i;
+    r.grid = grid;
     return r;
 }
 
-void slot_unissue(DevCtx *c, const SlotRef &r) {
+void slot_unissue(DevCtx *c, SlotRef &r) {
     if (r.idx < 0) return;
+    c->slot[r.idx].seq--;  // under the launch lock r still holds
+    r.lk.unlock();
     std::lock_guard<std::mutex> lk(g_mu);
-    c->slot[r.idx].issued--;
     c->slot[r.idx].issued_wgs -= r.grid;
 }
 
@@ -527,7 +533,7 @@ int launch_fixed(DevCtx *c, int idx, const void *pack, int width, int lg, const 
                              : KLaunch{crc64_batch_kernel<6, kFixedAligned, false, false, true>, Shape<64, kFixedAligned>::block,
                                        Shape<64, kFixedAligned>::blocks_per_cu};
         const unsigned grid = grid_for(c, (uint64_t)count << sl, k);
-        const SlotRef sr = queue_slot(c, stream, grid);
+        SlotRef sr = queue_slot(c, stream, grid);
         a.queue = sr.q;
         int rc = launch(k, a, grid, stream);
         if (rc != MCHECKSUM_GPU_OK) slot_unissue(c, sr);

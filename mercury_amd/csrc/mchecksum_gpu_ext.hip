@@ -869,7 +869,7 @@ int mchecksum_gpu_checksum_segments(const char *hash_method, const uint64_t *dev
     } else {
         // the aligned chunk pass takes the work queue; the ragged pass never
         // touches the slot (a.queue is cleared for it)
-        const SlotRef sr = MCK_SEG_QUEUE ? queue_slot(c, stream, 2u * (uint32_t)c->cus) : SlotRef{};
+        SlotRef sr = MCK_SEG_QUEUE ? queue_slot(c, stream, 2u * (uint32_t)c->cus) : SlotRef{};
         a.queue = sr.q;
         hipLaunchKernelGGL((seg_kernel<64, 1>), dim3(2 * c->cus), dim3(1024), 0, s, a);
         e = hipGetLastError();
@@ -992,7 +992,7 @@ int mchecksum_gpu_checksum_xdr(const char *hash_method, const mchecksum_xdr_fiel
         a.err_word = error_word();
         uint64_t blocks = (count + 15) / 16;
         if (blocks > (uint64_t)c->cus) blocks = (uint64_t)c->cus;
-        const SlotRef sr = queue_slot(c, stream, (uint32_t)blocks);
+        SlotRef sr = queue_slot(c, stream, (uint32_t)blocks);
         a.queue = sr.q;
         auto k = width == 32 ? (nt ? xdr_fast_kernel<32, true> : xdr_fast_kernel<32, false>)
                              : (nt ? xdr_fast_kernel<64, true> : xdr_fast_kernel<64, false>);

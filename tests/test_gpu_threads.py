@@ -70,3 +70,60 @@ def test_eight_host_threads_first_calls_together(gpu):
     r = subprocess.run([sys.executable, "-c", SCRIPT, ROOT], capture_output=True, text=True, timeout=110,
                        env=dict(os.environ, MCHECKSUM_GPU_LIGHT="0"))
     assert r.returncode == 0 and "threads ok" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
+
+
+SHARED = r"""
+import sys, threading
+import numpy as np
+import torch
+sys.path.insert(0, sys.argv[1])
+from mercury_amd import gpu as G
+from oracle import oracle as O
+host = O.splitmix_bytes(8 << 20, 4242)
+dev = torch.cat([torch.from_numpy(host).cuda(), torch.zeros(64, dtype=torch.uint8, device="cuda")])
+rng = np.random.default_rng(9)
+offs = np.zeros(3001, dtype=np.uint64)
+offs[1:] = np.cumsum(rng.integers(0, 2048, 3000))
+offs_d = torch.from_numpy(offs.astype(np.int64)).cuda()
+want = O.batch_offsets("crc32c", host, offs, nthreads=4)
+s = torch.cuda.Stream()  # ONE stream shared by every thread
+ITERS, NT = 60, 8
+outs = torch.zeros((NT, ITERS, 3000), dtype=torch.int32, device="cuda")
+torch.cuda.synchronize()
+barrier = threading.Barrier(NT)
+errors = []
+
+def worker(k):
+    try:
+        barrier.wait()
+        for it in range(ITERS):
+            G.checksum_offsets("crc32c", dev, offs_d, out=outs[k, it], stream=s)
+    except Exception as e:  # reported below
+        errors.append((k, repr(e)))
+
+th = [threading.Thread(target=worker, args=(k,)) for k in range(NT)]
+for t in th:
+    t.start()
+for t in th:
+    t.join(timeout=90)
+assert not any(t.is_alive() for t in th), "a worker thread did not finish"
+s.synchronize()
+assert not errors, errors[:5]
+w = torch.from_numpy(want.astype(np.uint32).view(np.int32)).cuda()
+bad = torch.nonzero((outs != w).any(dim=2)).tolist()
+assert not bad, bad[:8]
+assert G.queue_faults() == 0
+print("shared stream ok", G.queue_stats())
+"""
+
+
+def test_threads_sharing_one_stream_alternate_the_slot_banks(gpu):
+    """8 host threads launch 480 queue batches onto ONE stream at once: the
+    stream's slot alternates two banks (crc_gpu_device.h, "Two banks per
+    slot"), which is only sound if the launches reach the device in the order
+    their banks were handed out -- the slot's launch lock (queue_slot) holds
+    from the bank choice through the enqueue.  Every result is exact and no
+    queue wait gave up."""
+    r = subprocess.run([sys.executable, "-c", SHARED, ROOT], capture_output=True, text=True, timeout=110,
+                       env=dict(os.environ, MCHECKSUM_GPU_LIGHT="0"))
+    assert r.returncode == 0 and "shared stream ok" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
