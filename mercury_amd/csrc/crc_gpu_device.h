@@ -739,28 +739,43 @@ __device__ __forceinline__ uint32_t combine32(TAB lds, uint32_t s0, uint32_t s1,
 
 // LDS fill in 16-byte granules: a replicated entry's 4 neighbouring copies are
 // one ds_write_b128 of the same value (8 per thread at 1024 threads instead of
-// 32 dword loads + writes); the operator tables are copied as uint4.
+// 32 dword loads + writes); the operator tables are copied as uint4.  The
+// throughput layout issues every load of the fill (8 table entries, one
+// operator granule, one combine-operator granule per thread) before its first
+// write, so the fill costs one global round trip instead of three (round 2 ran
+// the three copies one after another, each behind its own wait).
 template <bool LIGHT, int BLOCK>
 __device__ void fill_lds32(uint8_t *lds, const crc32_gpu_pack_t *pk) {
     uint4 *l4 = reinterpret_cast<uint4 *>(lds);
+    const uint4 *ops = reinterpret_cast<const uint4 *>(&pk->ops[0][0][0]);
+    const uint32_t nops = pk->nops * 32u;
     if constexpr (LIGHT) {
         const uint4 *m = reinterpret_cast<const uint4 *>(&pk->main[0][0]);
         for (uint32_t q = threadIdx.x; q < 256u; q += BLOCK) l4[q] = m[q];
+        for (uint32_t q = threadIdx.x; q < nops; q += BLOCK) l4[kL32LightMain / 16 + q] = ops[q];
     } else {
-        for (uint32_t q = threadIdx.x; q < 8192u; q += BLOCK) {
-            const uint32_t d = q << 2;
+        static_assert(BLOCK == 1024 && CRC32_NOPS_MAX * 32 <= BLOCK, "one operator granule per thread");
+        const uint32_t t = threadIdx.x;
+        const uint4 *lv = reinterpret_cast<const uint4 *>(&pk->lv[0][0][0][0]);  // two-level combine operators
+        // loads in range of the pack's arrays whatever nops is (so none waits
+        // for the scalar load of nops), stores predicated
+        const uint32_t tc = t < CRC32_NOPS_MAX * 32u ? t : 0u, tl = t & 511u;
+        uint4 o = ops[tc];
+        const uint4 w = lv[tl];
+        uint32_t v[8];
+#pragma unroll
+        for (uint32_t i = 0; i < 8; i++) {
+            const uint32_t d = (t + i * BLOCK) << 2;
             const uint32_t region = d >> 14, e = (d >> 6) & 255u, half = (d >> 5) & 1u;
-            const uint32_t v = pk->main[2 * region + half][e];
-            l4[q] = make_uint4(v, v, v, v);
+            v[i] = pk->main[2 * region + half][e];
         }
-    }
-    const uint4 *ops = reinterpret_cast<const uint4 *>(&pk->ops[0][0][0]);
-    const uint32_t nops = pk->nops * 32u;
-    const uint32_t base = (LIGHT ? kL32LightMain : kL32Main) / 16;
-    for (uint32_t q = threadIdx.x; q < nops; q += BLOCK) l4[base + q] = ops[q];
-    if constexpr (!LIGHT) {  // two-level combine operators (used at G = 64)
-        const uint4 *lv = reinterpret_cast<const uint4 *>(&pk->lv[0][0][0][0]);
-        for (uint32_t q = threadIdx.x; q < 512u; q += BLOCK) l4[kL32Lv / 16 + q] = lv[q];
+        // keep the operator load up here with the others (the compiler would
+        // sink it into the predicated store below, behind a second round trip)
+        asm volatile("" : "+v"(o.x), "+v"(o.y), "+v"(o.z), "+v"(o.w));
+#pragma unroll
+        for (uint32_t i = 0; i < 8; i++) l4[t + i * BLOCK] = make_uint4(v[i], v[i], v[i], v[i]);
+        if (t < nops) l4[kL32Main / 16 + t] = o;
+        if (t < 512u) l4[kL32Lv / 16 + t] = w;
     }
 }
 
