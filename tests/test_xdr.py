@@ -168,3 +168,35 @@ def test_gpu_xdr_rejects_bad_schemas(gpu):
             gpu.checksum_xdr("crc32c", data, offs, bad)
     with pytest.raises(gpu.GpuChecksumError):
         gpu.checksum_xdr("crc16", data, offs, [(0, 4)])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", LAYOUTS)
+@pytest.mark.parametrize("method", ["crc32c", "crc64", "crc64-jones"])
+def test_gpu_xdr_fast_field_edges(gpu, oracle_mod, method, layout, monkeypatch):
+    """Field lengths around the throughput layout's step-loop threshold
+    (kXdrFastMin = 256: shorter fields take the byte walk, longer ones the
+    1 KiB step loop started from the running register), around the 1 KiB
+    step and the 128-B grid, at every start alignment mod 16 (a raw lead-in
+    of 0..15 bytes), and three large fields in one message (the register runs
+    from one step loop into the next): every CRC equal to the oracle's over
+    the hashed stream."""
+    monkeypatch.setenv("MCHECKSUM_GPU_XDR_FAST", layout)
+    O = oracle_mod
+    I, OPL, RAWL, OP = O.XDR_INT, O.XDR_OPAQUE_LEN, O.XDR_RAW_LEN, O.XDR_OPAQUE
+    rng = np.random.default_rng(31)
+    lens = [0, 1, 3, 4, 5, 7, 8, 9, 127, 128, 129, 252, 255, 256, 257, 260, 383, 384, 1020, 1023, 1024, 1025,
+            1151, 1152, 2047, 2048, 4099]
+    # lead-in length + bytes, the field under test, a fixed 300-B opaque, a raw tail
+    schema = [(I, 4), (RAWL, 0), (I, 4), (OPL, 0), (OP, 300), (I, 8), (RAWL, 0)]
+    msgs = []
+    for a in range(16):
+        for n in lens:
+            v = [a, rng.integers(0, 256, a, dtype=np.uint8).tobytes(), n,
+                 rng.integers(0, 256, n, dtype=np.uint8).tobytes(),
+                 rng.integers(0, 256, 300, dtype=np.uint8).tobytes(), 700 + a,
+                 rng.integers(0, 256, 700 + a, dtype=np.uint8).tobytes()]
+            msgs.append(O.xdr_encode(schema, v))
+    got = _run(gpu, method, msgs, schema)
+    want = [O.crc(method, O.xdr_hashed_stream(schema, m)) for m in msgs]
+    assert got.tolist() == want
