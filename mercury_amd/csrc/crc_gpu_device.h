@@ -411,7 +411,13 @@ __device__ bool wg_publish(WgQueue *L, uint32_t seq, uint64_t id, uint32_t cl) {
 // (the fetch's returning atomic waits for those adds to be performed: vmcnt
 // also counts non-returning atomics on gfx9-family parts).  Without a slot
 // (see "Exclusivity") the workgroup takes the static split (busy = 1).
-__device__ __attribute__((unused)) void wg_queue_init(WgQueue *L, unsigned long long *q, uint64_t n) {
+//
+// Split in two for kernels whose waves start on a static first unit
+// (for_each_unit<DYN, true>): wg_queue_reset (LDS only) before the barrier,
+// wg_queue_start after it -- the fetch's round trip then no longer sits in
+// front of thread 0's wave's table fill (waves look for a chunk only after
+// their first unit; until the publish they wait on the ring entry).
+__device__ __attribute__((unused)) void wg_queue_reset(WgQueue *L, unsigned long long *q) {
     L->slot = 0;
     L->drained = 0;
     L->exited = 0;
@@ -420,6 +426,8 @@ __device__ __attribute__((unused)) void wg_queue_init(WgQueue *L, unsigned long 
         L->reads[r] = 0;
         L->entry[r] = ~0ull;
     }
+}
+__device__ __attribute__((unused)) void wg_queue_start(WgQueue *L, unsigned long long *q, uint64_t n) {
     if (!q) return;
     if (blockIdx.x == 0) {
         unsigned long long *o = reinterpret_cast<unsigned long long *>(reinterpret_cast<uintptr_t>(q) ^ kQBankBytes);
@@ -428,6 +436,10 @@ __device__ __attribute__((unused)) void wg_queue_init(WgQueue *L, unsigned long 
     }
     const ChunkPlan plan(n);
     (void)wg_publish(L, 0, wg_fetch(L, q, plan.nch), plan.cl);
+}
+__device__ __attribute__((unused)) void wg_queue_init(WgQueue *L, unsigned long long *q, uint64_t n) {
+    wg_queue_reset(L, q);
+    wg_queue_start(L, q, n);
 }
 
 template <typename T>
@@ -466,7 +478,14 @@ __device__ __forceinline__ void slot_exit(unsigned long long *queue, uint32_t *w
 #ifndef MCK_QFAULT_TEST
 #define MCK_QFAULT_TEST 0
 #endif
-template <bool DYN, class F>
+//
+// FIRST: the caller has already run each wave's first unit, `wave` itself
+// (known at kernel entry, so its loads can go out before the LDS fill); the
+// static cursor starts at wave + nw and the queue deals units [q0, n),
+// q0 = min(n, nw) -- wg_queue_init gets n - q0 (first_static_units).
+__device__ __forceinline__ uint64_t first_static_units(uint64_t n, uint32_t nw) { return n < nw ? n : nw; }
+
+template <bool DYN, bool FIRST = false, class F>
 __device__ __forceinline__ bool for_each_unit(WgQueue *L, unsigned long long *queue, uint64_t n, uint32_t wave,
                                               uint32_t nw, F &&body) {
     if constexpr (DYN) {
@@ -474,12 +493,13 @@ __device__ __forceinline__ bool for_each_unit(WgQueue *L, unsigned long long *qu
         // payload loop made the offsets kernels spill, and so does the copy
         // loop unswitching makes -- hence busy is re-read from LDS every
         // iteration (an atomic load the compiler cannot hoist).
-        uint64_t su = wave;  // static cursor (busy slot)
+        const uint64_t q0 = FIRST ? first_static_units(n, nw) : 0;
+        uint64_t su = FIRST ? (uint64_t)wave + nw : wave;  // static cursor (busy slot)
         const bool l0 = (threadIdx.x & 63u) == 0;
 #ifndef MCK_QLEAD_DIV
 #define MCK_QLEAD_DIV 4
 #endif
-        const ChunkPlan plan(n);
+        const ChunkPlan plan(n - q0);
         const uint32_t cl = plan.cl, cu = 1u << cl, lead = cu > MCK_QLEAD_DIV ? cu / MCK_QLEAD_DIV : 1;
         const uint64_t nch = plan.nch;
 #if MCK_TRACE
@@ -557,7 +577,7 @@ __device__ __forceinline__ bool for_each_unit(WgQueue *L, unsigned long long *qu
                 if (id == kNoChunk) break;
                 // every chunk spans cu slots; a tail chunk's slots past its size are skipped
                 const uint32_t k = t & (cu - 1);
-                u = k < plan.size(id) ? plan.start(id) + k : n;
+                u = k < plan.size(id) ? q0 + plan.start(id) + k : n;
             }
 #if MCK_TRACE
             const unsigned long long b0 = wall_clock64();
@@ -588,7 +608,7 @@ __device__ __forceinline__ bool for_each_unit(WgQueue *L, unsigned long long *qu
         (void)nw;
         return __builtin_amdgcn_readfirstlane(first) != 0;
     } else {
-        for (uint64_t u = wave; u < n; u += nw) body(u);
+        for (uint64_t u = FIRST ? (uint64_t)wave + nw : wave; u < n; u += nw) body(u);
         return false;
     }
 }
@@ -744,12 +764,19 @@ __device__ __forceinline__ uint32_t combine32(TAB lds, uint32_t s0, uint32_t s1,
 // operator granule, one combine-operator granule per thread) before its first
 // write, so the fill costs one global round trip instead of three (round 2 ran
 // the three copies one after another, each behind its own wait).
-template <bool LIGHT, int BLOCK>
-__device__ void fill_lds32(uint8_t *lds, const crc32_gpu_pack_t *pk) {
+// `issue` runs between the fill's loads and its LDS writes (the kernel's
+// first-payload prefetch: issued after the table loads, it does not delay
+// their writes).
+struct NoIssue {
+    __device__ void operator()() const {}
+};
+template <bool LIGHT, int BLOCK, class F = NoIssue>
+__device__ void fill_lds32(uint8_t *lds, const crc32_gpu_pack_t *pk, F &&issue = F{}) {
     uint4 *l4 = reinterpret_cast<uint4 *>(lds);
     const uint4 *ops = reinterpret_cast<const uint4 *>(&pk->ops[0][0][0]);
     const uint32_t nops = pk->nops * 32u;
     if constexpr (LIGHT) {
+        issue();
         const uint4 *m = reinterpret_cast<const uint4 *>(&pk->main[0][0]);
         for (uint32_t q = threadIdx.x; q < 256u; q += BLOCK) l4[q] = m[q];
         for (uint32_t q = threadIdx.x; q < nops; q += BLOCK) l4[kL32LightMain / 16 + q] = ops[q];
@@ -772,6 +799,7 @@ __device__ void fill_lds32(uint8_t *lds, const crc32_gpu_pack_t *pk) {
         // keep the operator load up here with the others (the compiler would
         // sink it into the predicated store below, behind a second round trip)
         asm volatile("" : "+v"(o.x), "+v"(o.y), "+v"(o.z), "+v"(o.w));
+        issue();
 #pragma unroll
         for (uint32_t i = 0; i < 8; i++) l4[t + i * BLOCK] = make_uint4(v[i], v[i], v[i], v[i]);
         if (t < nops) l4[kL32Main / 16 + t] = o;
@@ -788,6 +816,9 @@ __device__ void fill_lds32(uint8_t *lds, const crc32_gpu_pack_t *pk) {
 #endif
 #ifndef MCK_LA32
 #define MCK_LA32 1
+#endif
+#ifndef MCK_PREFETCH32
+#define MCK_PREFETCH32 1
 #endif
 // Global-address-space views: loads through them are global_load (never
 // flat_load, which would also count against lgkmcnt and make every LDS wait
@@ -815,18 +846,28 @@ __device__ __forceinline__ uint4 ldg16(gbyte_t p) {
 // saddr loads with the lane offset in one VGPR and the slot in the immediate).
 // Each slot's data word is folded into the state before the slot is reloaded,
 // so the ring needs no register copies.
+// The first kRing steps of a payload (every one in range: K >= kRing).
+template <int LOG2G, bool NT>
+__device__ __forceinline__ void ring32_load(uint4 (&ring)[kRing], const uint8_t *p, uint32_t gl) {
+    constexpr uint32_t S = 16u << LOG2G;
+    const gbyte_t lb = global_ptr(p, LOG2G == 6);
+#pragma unroll
+    for (uint32_t u = 0; u < kRing; u++) ring[u] = ldg16<NT>(lb + (16u * gl + u * S));
+}
+
+// loaded: ring already holds the payload's first kRing steps (ring32_load,
+// issued by the kernel before its LDS fill for the wave's first payload).
 template <int LOG2G, bool NT, class TAB>
 __device__ __forceinline__ uint32_t payload32_aligned(TAB lds, const uint8_t *p, uint64_t K64, uint32_t gl,
-                                                      uint32_t lc0, uint32_t lc1, uint32_t init) {
+                                                      uint32_t lc0, uint32_t lc1, uint32_t init,
+                                                      uint4 (&ring)[kRing], bool loaded) {
     constexpr uint32_t G = 1u << LOG2G;
     constexpr uint32_t R = kRing;
     constexpr uint32_t S = 16u * G;  // bytes per step
     const uint32_t K = (uint32_t)K64;
     gbyte_t lb = global_ptr(p, LOG2G == 6);
     const uint32_t lo = 16u * gl;
-    uint4 ring[R];
-#pragma unroll
-    for (uint32_t u = 0; u < R; u++) ring[u] = ldg16<NT>(lb + (lo + u * S));
+    if (!loaded) ring32_load<LOG2G, NT>(ring, p, gl);
     lb += R * S;
     uint32_t x0 = gl == 0 ? init : 0u, x1 = 0, x2 = 0, x3 = 0;
 #if MCK_LA32
@@ -884,7 +925,8 @@ __device__ __forceinline__ uint32_t payload32_aligned(TAB lds, const uint8_t *p,
 #else
 template <int LOG2G, bool NT, class TAB>
 __device__ __forceinline__ uint32_t payload32_aligned(TAB lds, const uint8_t *p, uint64_t K, uint32_t gl,
-                                                      uint32_t lc0, uint32_t lc1, uint32_t init) {
+                                                      uint32_t lc0, uint32_t lc1, uint32_t init,
+                                                      uint4 (&)[kRing], bool) {
     constexpr int G = 1 << LOG2G;
     const uint4 *src = reinterpret_cast<const uint4 *>(p) + gl;
     uint4 ring[kRing];
@@ -908,6 +950,12 @@ __device__ __forceinline__ uint32_t payload32_aligned(TAB lds, const uint8_t *p,
     return combine32<LOG2G>(lds, x0, x1, x2, x3, gl);
 }
 #endif
+template <int LOG2G, bool NT, class TAB>
+__device__ __forceinline__ uint32_t payload32_aligned(TAB lds, const uint8_t *p, uint64_t K, uint32_t gl,
+                                                      uint32_t lc0, uint32_t lc1, uint32_t init) {
+    uint4 ring[kRing];
+    return payload32_aligned<LOG2G, NT>(lds, p, K, gl, lc0, lc1, init, ring, false);
+}
 
 // Any alignment, any length (0 included).  Per-lane window; the wave loops to
 // the largest step count of its groups.
@@ -1153,21 +1201,43 @@ __global__ __launch_bounds__(kBlk32<LIGHT>, 1) void crc32c_batch_kernel(BatchArg
 #if defined(MCK_EMPTY) && MCK_EMPTY == 2
     if (!DYN) return;  // diagnostic: launch cost alone
 #endif
-    if (DYN && threadIdx.x == 0) wg_queue_init(&wgq, a.queue, units);
-    fill_lds32<LIGHT, kBlk32<LIGHT>>(lds_raw, pk);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t gl = lane & ((1u << LOG2G) - 1u), grp = lane >> LOG2G;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
+    const uint32_t nw = gridDim.x * kWavesPerBlock;
+    // Aligned batches: the loads of the wave's first payload go out before the
+    // LDS table fill, so their HBM round trip overlaps the fill's (the first
+    // unit is static on the queue path too: for_each_unit<DYN, PRE>).
+    constexpr bool PRE = MODE == kFixedAligned && !LIGHT && MCK_ALIGNED32_V2 && (DYN ? MCK_PREFETCH32 >= 2 : MCK_PREFETCH32 >= 1);
+    constexpr bool LATE_START = PRE && DYN && MCK_PREFETCH32 == 2;
+    // model words read once, ahead of any store (scalar loads; read after the
+    // barrier they became a vector load per payload whose wait, merged with
+    // the ring's at the prefetch branch, cost a vmcnt(0) per payload)
+    const uint32_t init = pk->init, xorout = pk->xorout;
+    uint4 ring0[kRing];
+    const bool pre = PRE && wave < units;
+    if (DYN && threadIdx.x == 0) {
+        if (LATE_START) wg_queue_reset(&wgq, a.queue);
+        else wg_queue_init(&wgq, a.queue, PRE ? units - first_static_units(units, nw) : units);
+    }
+    fill_lds32<LIGHT, kBlk32<LIGHT>>(lds_raw, pk, [&] {
+        // unconditional (a wave without a first unit reads the last payload's
+        // first steps): loads under a branch leave the waitcnt pass a merge
+        // point, where it falls back to vmcnt(0) for the fill's writes
+        if constexpr (PRE) {
+            const uint64_t p = (uint64_t)wave * PPW + grp;
+            ring32_load<LOG2G, NT>(ring0, a.base + (p < a.count ? p : a.count - 1) * a.stride, gl);
+        }
+    });
     __syncthreads();
+    if (LATE_START && threadIdx.x == 0) wg_queue_start(&wgq, a.queue, units - first_static_units(units, nw));
 #if defined(MCK_EMPTY) && MCK_EMPTY == 1
     if (!DYN) return;  // diagnostic: launch + LDS table fill
 #endif
     MCK_STAMP(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6), 1);
     const Tab32<LIGHT> lds{lds_raw};
 
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t gl = lane & ((1u << LOG2G) - 1u), grp = lane >> LOG2G;
     const uint32_t lc0 = (lane & 31u) << 2, lc1 = lc0 | 0x10000u;
-    const uint32_t xorout = pk->xorout;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
-    const uint32_t nw = gridDim.x * kWavesPerBlock;
 
     if (MODE == kOffsets) {
         auto one = [&](uint64_t p) {
@@ -1198,17 +1268,24 @@ __global__ __launch_bounds__(kBlk32<LIGHT>, 1) void crc32c_batch_kernel(BatchArg
         MCK_STAMP(wave, 2);
         return;
     }
-    const bool faulted = for_each_unit<DYN>(&wgq, a.queue, units, wave, nw, [&](uint64_t u) {
+    auto unit = [&](uint64_t u, bool loaded) {
         const uint64_t p = u * PPW + grp;
         const bool act = p < a.count;
         const uint64_t pc = act ? p : a.count - 1;
         uint32_t x;
         if (MODE == kFixedAligned)
-            x = payload32_aligned<LOG2G, NT>(lds, a.base + pc * a.stride, a.len >> (4 + LOG2G), gl, lc0, lc1, pk->init);
+            x = payload32_aligned<LOG2G, NT>(lds, a.base + pc * a.stride, a.len >> (4 + LOG2G), gl, lc0, lc1, init, ring0,
+                                             loaded);
         else
             x = payload32_generic<LOG2G, NT>(lds, pk, a.base + pc * a.stride, a.len, gl, lc0, lc1);
         if (act && gl == 0) emit<uint32_t, VERIFY>(a, p, x ^ xorout);
-    });
+    };
+    // The prefetched first unit runs in a copy of the payload loop of its own:
+    // one copy behind a loaded/not-loaded branch leaves the prefetch loads
+    // pending at the loop head in the waitcnt pass's view, and it then waited
+    // vmcnt(0) -- the previous payload's CRC store included -- at every payload.
+    if (PRE && pre) unit(wave, true);
+    const bool faulted = for_each_unit<DYN, PRE>(&wgq, a.queue, units, wave, nw, [&](uint64_t u) { unit(u, false); });
     if (faulted) fail_closed<VERIFY>(a);
     MCK_STAMP(wave, 2);
 }
