@@ -776,10 +776,23 @@ __device__ void fill_lds32(uint8_t *lds, const crc32_gpu_pack_t *pk, F &&issue =
     const uint4 *ops = reinterpret_cast<const uint4 *>(&pk->ops[0][0][0]);
     const uint32_t nops = pk->nops * 32u;
     if constexpr (LIGHT) {
+        // all loads (one main-table granule, up to three operator granules per
+        // thread) before the first write: one global round trip, not two
+        static_assert(BLOCK == 256 && CRC32_NOPS_MAX * 32 <= 3 * BLOCK, "fill granules per thread");
         issue();
         const uint4 *m = reinterpret_cast<const uint4 *>(&pk->main[0][0]);
-        for (uint32_t q = threadIdx.x; q < 256u; q += BLOCK) l4[q] = m[q];
-        for (uint32_t q = threadIdx.x; q < nops; q += BLOCK) l4[kL32LightMain / 16 + q] = ops[q];
+        const uint32_t t = threadIdx.x;
+        const uint4 mv = m[t];
+        auto op_at = [&](uint32_t q) { return ops[q < CRC32_NOPS_MAX * 32u ? q : 0u]; };
+        uint4 o0 = op_at(t), o1 = op_at(t + BLOCK), o2 = op_at(t + 2 * BLOCK);
+        // (pinned after all four loads are out: the compiler sank each
+        // operator load into its predicated store, one round trip apiece)
+        asm volatile("" : "+v"(o0.x), "+v"(o0.y), "+v"(o0.z), "+v"(o0.w), "+v"(o1.x), "+v"(o1.y), "+v"(o1.z),
+                     "+v"(o1.w), "+v"(o2.x), "+v"(o2.y), "+v"(o2.z), "+v"(o2.w));
+        l4[t] = mv;
+        if (t < nops) l4[kL32LightMain / 16 + t] = o0;
+        if (t + BLOCK < nops) l4[kL32LightMain / 16 + t + BLOCK] = o1;
+        if (t + 2 * BLOCK < nops) l4[kL32LightMain / 16 + t + 2 * BLOCK] = o2;
     } else {
         static_assert(BLOCK == 1024 && CRC32_NOPS_MAX * 32 <= BLOCK, "one operator granule per thread");
         const uint32_t t = threadIdx.x;
@@ -819,6 +832,9 @@ __device__ void fill_lds32(uint8_t *lds, const crc32_gpu_pack_t *pk, F &&issue =
 #endif
 #ifndef MCK_PREFETCH32
 #define MCK_PREFETCH32 1
+#endif
+#ifndef MCK_PREFETCH32_LIGHT
+#define MCK_PREFETCH32_LIGHT 0
 #endif
 // Global-address-space views: loads through them are global_load (never
 // flat_load, which would also count against lgkmcnt and make every LDS wait
@@ -1208,7 +1224,8 @@ __global__ __launch_bounds__(kBlk32<LIGHT>, 1) void crc32c_batch_kernel(BatchArg
     // Aligned batches: the loads of the wave's first payload go out before the
     // LDS table fill, so their HBM round trip overlaps the fill's (the first
     // unit is static on the queue path too: for_each_unit<DYN, PRE>).
-    constexpr bool PRE = MODE == kFixedAligned && !LIGHT && MCK_ALIGNED32_V2 && (DYN ? MCK_PREFETCH32 >= 2 : MCK_PREFETCH32 >= 1);
+    constexpr bool PRE = MODE == kFixedAligned && (!LIGHT || MCK_PREFETCH32_LIGHT) && MCK_ALIGNED32_V2 &&
+                         (DYN ? MCK_PREFETCH32 >= 2 : MCK_PREFETCH32 >= 1);
     constexpr bool LATE_START = PRE && DYN && MCK_PREFETCH32 == 2;
     // model words read once, ahead of any store (scalar loads; read after the
     // barrier they became a vector load per payload whose wait, merged with
@@ -1221,12 +1238,16 @@ __global__ __launch_bounds__(kBlk32<LIGHT>, 1) void crc32c_batch_kernel(BatchArg
         else wg_queue_init(&wgq, a.queue, PRE ? units - first_static_units(units, nw) : units);
     }
     fill_lds32<LIGHT, kBlk32<LIGHT>>(lds_raw, pk, [&] {
-        // unconditional (a wave without a first unit reads the last payload's
-        // first steps): loads under a branch leave the waitcnt pass a merge
-        // point, where it falls back to vmcnt(0) for the fill's writes
+        // Throughput layout: unconditional (a wave without a first unit reads
+        // the last payload's first steps) -- loads under a branch leave the
+        // waitcnt pass a merge point, where it falls back to vmcnt(0) for the
+        // fill's writes.  Light layout (small batches: most of its 8192 waves
+        // may have no unit): only waves with a first unit load, and before the
+        // fill's loads (fill_lds32 runs `issue` first there), so the fill's
+        // waits count the same on both paths.
         if constexpr (PRE) {
             const uint64_t p = (uint64_t)wave * PPW + grp;
-            ring32_load<LOG2G, NT>(ring0, a.base + (p < a.count ? p : a.count - 1) * a.stride, gl);
+            if (!LIGHT || pre) ring32_load<LOG2G, NT>(ring0, a.base + (p < a.count ? p : a.count - 1) * a.stride, gl);
         }
     });
     __syncthreads();

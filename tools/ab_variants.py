@@ -27,6 +27,12 @@ SHAPES = {
     "c4_64": ("crc64", 262144, None, 0x4D43310000000004),
     "seg": ("crc64", 8192, "seg", 0x4D43310000000003),      # bench.py's segments layout
     "seg32": ("crc32c", 8192, "seg", 0x4D43310000000003),   # the same layout, CRC-32C
+    # small batches (per-call latency; the light layout up to 16 MiB)
+    "s1": ("crc32c", 1, 4096, 0x4D43310000000002),
+    "s64": ("crc32c", 64, 4096, 0x4D43310000000002),
+    "s1024": ("crc32c", 1024, 4096, 0x4D43310000000002),
+    "s4096": ("crc32c", 4096, 4096, 0x4D43310000000002),
+    "s1_64k": ("crc32c", 1, 65536, 0x4D43310000000002),
 }
 
 
