@@ -33,6 +33,8 @@ SHAPES = {
     "s1024": ("crc32c", 1024, 4096, 0x4D43310000000002),
     "s4096": ("crc32c", 4096, 4096, 0x4D43310000000002),
     "s1_64k": ("crc32c", 1, 65536, 0x4D43310000000002),
+    "c64s1": ("crc64", 1, 4096, 0x4D43310000000003),
+    "c64s1024": ("crc64", 1024, 4096, 0x4D43310000000003),
 }
 
 
