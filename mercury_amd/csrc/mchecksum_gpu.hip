@@ -420,7 +420,8 @@ constexpr uint64_t kMaxUnits = 1ull << 31;
 int do_offsets(const char *method, const void *base, const uint64_t *offsets, size_t count, void *out,
                const void *expected, uint8_t *status, uint32_t *mism, void *stream, bool verify,
                bool msg = false, size_t pay_off = 0, size_t hash_off = 0) {
-    if ((!base && count) || !offsets || (!verify && !out && count) || (verify && !msg && !expected))
+    // an empty batch needs no buffers (not even the one-entry offsets table)
+    if (count && (!base || !offsets || (!verify && !out) || (verify && !msg && !expected)))
         return set_err(MCHECKSUM_GPU_EINVAL, "NULL pointer argument");
     if (msg && (hash_off + 4 > pay_off || pay_off > (1u << 30)))
         return set_err(MCHECKSUM_GPU_EINVAL, "hash_offset + 4 must not exceed payload_offset");
