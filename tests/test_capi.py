@@ -105,8 +105,12 @@ def test_batch_arguments_rejected_before_any_device_work(product_lib):
     for call, why in cases:
         assert call() == -1, why
         assert why.encode() in L.mchecksum_gpu_last_error(), (why, L.mchecksum_gpu_last_error())
-    # an empty batch is valid with NULL buffers
+    # an empty batch is valid with NULL buffers (the offsets table included):
+    # never EINVAL -- 0 with a device, ENODEV without one
     assert L.mchecksum_gpu_checksum_fixed(b"crc32c", None, 0, 0, 0, None, None) in (0, -2)
+    assert L.mchecksum_gpu_checksum_offsets(b"crc32c", None, None, 0, None, None) in (0, -2)
+    assert L.mchecksum_gpu_verify_offsets(b"crc64", None, None, 0, None, None, None, None) in (0, -2)
+    assert L.mchecksum_gpu_verify_messages(b"crc32c", None, None, 0, 20, 16, None, None, None) in (0, -2)
 
 
 def test_lanes_per_payload_heuristic(product_lib):
