@@ -1221,9 +1221,12 @@ __global__ __launch_bounds__(kBlk32<LIGHT>, 1) void crc32c_batch_kernel(BatchArg
     const uint32_t gl = lane & ((1u << LOG2G) - 1u), grp = lane >> LOG2G;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
     const uint32_t nw = gridDim.x * kWavesPerBlock;
-    // Aligned batches: the loads of the wave's first payload go out before the
-    // LDS table fill, so their HBM round trip overlaps the fill's (the first
-    // unit is static on the queue path too: for_each_unit<DYN, PRE>).
+    // Aligned batches on the static split (C2): the loads of the wave's first
+    // payload go out inside the LDS table fill, so their HBM round trip
+    // overlaps the fill's.  The queue path (the headline) keeps its first unit
+    // dynamic: a static first unit there (MCK_PREFETCH32 >= 2, for_each_unit
+    // <DYN, true>) measured 1% slower; the
+    // light layout gains nothing from it (MCK_PREFETCH32_LIGHT).
     constexpr bool PRE = MODE == kFixedAligned && (!LIGHT || MCK_PREFETCH32_LIGHT) && MCK_ALIGNED32_V2 &&
                          (DYN ? MCK_PREFETCH32 >= 2 : MCK_PREFETCH32 >= 1);
     constexpr bool LATE_START = PRE && DYN && MCK_PREFETCH32 == 2;
