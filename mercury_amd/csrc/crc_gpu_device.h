@@ -366,12 +366,22 @@ constexpr uint32_t kSpinMax = 1u << 24;
         break;                            \
     }
 
+#ifndef MCK_STEAL_ROT
+#define MCK_STEAL_ROT 0
+#endif
 // One lane: the next global chunk id for this workgroup, or kNoChunk.
 __device__ uint64_t wg_fetch(WgQueue *L, unsigned long long *q, uint64_t nch) {
     const uint32_t home = blockIdx.x % kQSub;
     uint32_t d = lds_ld(&L->drained);
     while (d < kQSub) {
+#if MCK_STEAL_ROT
+        // thieves of one home start at different victims (a rotation of the
+        // other seven by workgroup), so a drained XCD's 32 workgroups do not
+        // all queue on the next sub-queue's counter at the end of the batch
+        const uint32_t k = d == 0 ? home : (home + 1 + (d - 1 + (blockIdx.x / kQSub) % (kQSub - 1)) % (kQSub - 1)) % kQSub;
+#else
         const uint32_t k = (home + d) % kQSub;
+#endif
         // sub-queue k owns chunks k, k + 8, k + 16, ...: every XCD streams
         // from the same moving window of the batch (contiguous per-XCD ranges
         // -- 8 windows far apart -- measured 8% slower on the headline batch)
