@@ -367,7 +367,7 @@ constexpr uint32_t kSpinMax = 1u << 24;
     }
 
 #ifndef MCK_STEAL_ROT
-#define MCK_STEAL_ROT 0
+#define MCK_STEAL_ROT 1
 #endif
 // One lane: the next global chunk id for this workgroup, or kNoChunk.
 __device__ uint64_t wg_fetch(WgQueue *L, unsigned long long *q, uint64_t nch) {

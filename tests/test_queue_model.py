@@ -135,7 +135,9 @@ def _launch(spec, bank, rnd, res):
         home = b % QSUB
         d = L.drained
         while d < QSUB:
-            k = (home + d) % QSUB
+            # crc_gpu_device.h MCK_STEAL_ROT: a workgroup's victims after its
+            # home are the other seven rotated by (b / QSUB) % 7
+            k = home if d == 0 else (home + 1 + (d - 1 + (b // QSUB) % (QSUB - 1)) % (QSUB - 1)) % QSUB
             t = cur.sub[k]
             cur.sub[k] += 1
             yield
