@@ -20,7 +20,7 @@ GOBJS     := $(BUILD)/mchecksum_gpu.o $(BUILD)/mchecksum_gpu_ext.o
 
 QFAULTLIB := $(BUILD)/libmchecksum_qfault.so
 
-all: $(LIB) $(BENCHLIB) oracle $(BUILD)/c1_bench $(QFAULTLIB)
+all: $(LIB) $(BENCHLIB) oracle $(BUILD)/c1_bench $(QFAULTLIB) $(BUILD)/libcpu_batch.so
 
 $(BUILD) $(LIBDIR):
 	mkdir -p $@
@@ -61,6 +61,11 @@ oracle:
 
 $(BUILD)/c1_bench: tools/c1_bench.c include/mchecksum.h $(LIB) | $(BUILD)
 	$(CC) -O2 -std=c11 -Wall -Iinclude $< -o $@ -L$(LIBDIR) -lmchecksum -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)'
+
+# bench.py's cpu_baseline "product" leg: the streaming API over a batch on n threads
+$(BUILD)/libcpu_batch.so: tools/cpu_batch.c include/mchecksum.h $(LIB) | $(BUILD)
+	$(CC) -O2 -std=c11 -Wall -Wextra -fPIC -shared -fvisibility=hidden -Iinclude $< -o $@ -L$(LIBDIR) -lmchecksum \
+	  -lpthread -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)'
 
 # CPU-only artefacts (no hipcc needed): streaming API for host tests.
 cpu: $(LIBDIR)/libmchecksum_cpu.so

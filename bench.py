@@ -8,8 +8,12 @@ per-GPU batch (65536 payloads of 64 KiB = 4 GiB), inputs already in HBM.
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N,
 or bench.py --gpus N, which starts those ranks itself): each rank owns a
 contiguous share of ONE global batch, generated on its own device; no
-collective in the timed region.  After timing: RCCL all_gather of the
-per-share CRC arrays (global payload order) and of the timings.
+collective in the timed region.  By default every rank's share is the
+headline's 65536 x 64 KiB (weak scaling: the global batch is N x 4 GiB), so
+the 1/2/4/8 series is one per-GPU workload; --config c5 splits C5's fixed
+2^20 x 64 KiB batch instead (strong).  After timing: RCCL all_gather of the
+per-share CRC arrays (global payload order) and of the timings.  Under
+torchrun the process group is formed at every world size, 1 included.
 
 Prints ONE JSON line on rank 0 (contract in the task statement), with
 `roofline` (HIP-event kernel time vs HBM peak; `traffic` from the committed
@@ -73,8 +77,8 @@ def parse():
     # 0.62 -> 0.75 -> 0.62 ms over the first 30, profiles/r01/launch_series_metric.json)
     p.add_argument("--warmup", type=int, default=40)
     p.add_argument("--config", default=None, choices=sorted(CONFIGS),
-                   help="default: the headline (metric) at 1 GPU, C5's 2^20 x 64 KiB global batch split over "
-                        "the ranks at N > 1")
+                   help="default: the headline (metric), 65536 x 64 KiB per GPU at every N (weak scaling); "
+                        "c5 = C5's 2^20 x 64 KiB global batch split over the ranks (strong scaling)")
     p.add_argument("--streams", type=int, default=1,
                    help="issue consecutive steps round-robin on this many streams (independent batches, "
                         "fixed and offsets layouts)")
@@ -117,7 +121,9 @@ def main():
     if args.gpus < 1:
         sys.exit("bench.py: --gpus must be >= 1")
     if args.config is None:
-        args.config = "metric" if args.gpus == 1 else "c5"
+        # every N runs the headline's per-GPU batch (65536 x 64 KiB per rank,
+        # weak scaling), so the driver's 1/2/4/8 series is one workload
+        args.config = "metric"
     if CONFIGS[args.config][4] == "cpu":
         return bench_c1(args)
     import torch
@@ -126,7 +132,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    # Under torchrun (WORLD_SIZE set) the process group is formed at every
+    # world size, 1 included: `torchrun --nproc-per-node 1 bench.py` runs the
+    # same RCCL calls as the 8-GPU run (init, all_gather, all_reduce).
+    dist_on = env_world is not None
+    if dist_on:
         torch.cuda.set_device(local % torch.cuda.device_count())
         # The communication libraries may print connection notices on file
         # descriptor 1 (gloo's "[Gloo] Rank 0 is connected to ..."), which
@@ -262,7 +272,7 @@ def main():
     # two timestamp packets between consecutive kernels: +2.6 us on C2's
     # 42.2 us launches (rocprofv3 kernel trace, profiles/r02/c2_kernel_steady.json).
     ev_start, ev_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -277,7 +287,7 @@ def main():
         streams[0].wait_event(joined)
     ev_end.record(streams[0])
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     wall = time.perf_counter() - t0
     kern_ms = ev_start.elapsed_time(ev_end) / args.steps
@@ -285,7 +295,7 @@ def main():
     coll_dev = dev if args.backend == "nccl" else torch.device("cpu")
     t = torch.tensor([wall, kern_ms], dtype=torch.float64, device=coll_dev)
     per_rank = [t.clone() for _ in range(world)]
-    if world > 1:
+    if dist_on:
         dist.all_gather(per_rank, t)
     per_rank = [[float(x[0]), float(x[1])] for x in per_rank]
     wall_max = max(w for w, _ in per_rank)
@@ -307,7 +317,7 @@ def main():
         verify_note = (f"{args.steps + args.warmup + 1} verify launches: {bad_before} mismatches; one flipped bit "
                        f"flagged {flagged} (expected [{victim}])")
         crcs = sender  # the sender-side CRCs, checked against the oracle below
-    if world > 1:
+    if dist_on:
         # RCCL all_gather of the per-rank CRC arrays (padded to the largest
         # shard: ranks may hold different counts), then trimmed in rank order:
         # the global batch's CRCs in global payload order (messages: the
@@ -319,7 +329,7 @@ def main():
     got = G.as_unsigned(crcs) if rank == 0 else None
 
     bytes_all = torch.tensor([float(payload_bytes)], dtype=torch.float64, device=coll_dev)
-    if world > 1:
+    if dist_on:
         dist.all_reduce(bytes_all)
     total_bytes = float(bytes_all[0]) * args.steps  # every rank checksummed its shard once per step
     gib_s = total_bytes / wall_max / 2**30
@@ -338,9 +348,10 @@ def main():
             global_count=global_count, count=count, plan=plan, payload_bytes=payload_bytes, alg_bytes=alg_bytes,
             gib_s=gib_s, wall_max=wall_max, kern_ms_max=kern_ms_max, achieved=achieved, per_rank=per_rank,
             world=world, got=got, offsets_host=offsets_host, verify_note=verify_note,
+            process_group=dist.get_backend() if dist_on else None,
             lanes=G.lanes_per_payload(method, length or 65536) if layout == "fixed" else 64))
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if dist_on:
         dist.barrier()
         dist.destroy_process_group()
     return result
@@ -353,13 +364,15 @@ def report(args, r):
     traffic, traffic_src = pmc_traffic(r.config, r.world, r.alg_bytes)
     metric = {"metric": "GiB/s checksummed (device-resident), CRC32c, 64K x 64 KiB payloads",
               "c5": "GiB/s checksummed (device-resident), CRC32c, 1M x 64 KiB payloads split over the GPUs (C5)"}
-    workload = (f"{r.config}: {r.method} over {r.global_count} x {r.length if r.length else 'U[64B,64KiB]'} B payloads"
+    per_gpu = r.global_count // r.world if not r.strong else r.global_count
+    workload = (f"{r.config}: {r.method} over {per_gpu if not r.strong else r.global_count} x "
+                f"{r.length if r.length else 'U[64B,64KiB]'} B payloads"
                 + (" (offsets table)" if r.layout == "offsets" else "")
                 + (" as Mercury messages, verified in place" if r.layout == "messages" else "")
                 + (" as hg_perf_proc_iovec messages in XDR mode" if r.layout == "xdr" else "")
                 + (f" ({SEGS_PER_OBJECT} scattered segments each)" if r.layout == "segments" else "")
-                + (f", one global batch split over {r.world} GPUs" if r.world > 1 and r.layout != "segments"
-                   else ", per GPU" if r.world > 1 else ""))
+                + (f", one global batch split over {r.world} GPUs" if r.world > 1 and r.strong
+                   else f" per GPU ({r.global_count} in all over {r.world} GPUs)" if r.world > 1 else ""))
     result = {
         "metric": metric.get(r.config, f"GiB/s checksummed (device-resident), {r.config}"),
         "value": round(r.gib_s, 2),
@@ -377,6 +390,7 @@ def report(args, r):
                    "payloads_rank0": r.count, "payload_bytes": r.length, "bytes_rank0": r.payload_bytes,
                    "lanes_per_payload": r.lanes, "parallelism": f"shard{r.world}"},
         "world_size": r.world,
+        "process_group": getattr(r, "process_group", None),
         "per_rank": [{"rank": i, "wall_ms_per_step": round(w / args.steps * 1e3, 4), "kernel_ms": round(k, 4)}
                      for i, (w, k) in enumerate(r.per_rank)],
         "roofline": {"bound": "hbm", "achieved": round(r.achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -504,6 +518,7 @@ def cpu_baseline(method, seed, length, offsets_host, got, budget_s, samples, seg
         n = min(256, count0)
         host = np.concatenate([_segment_object_bytes(O, seed, length, j, slots) for j in range(n)])
         runv = lambda k, v, th: O.batch_fixed(method, host, length, length, k, variant=v, nthreads=th)  # noqa: E731
+        prod = lambda th: product_batch(method, host, th, count=n, length=length)  # noqa: E731
         sample_bytes = n * length
         what = f"the first {n} objects ({SEGS_PER_OBJECT} x {length // SEGS_PER_OBJECT} B segments, gathered)"
     elif xdr:
@@ -520,6 +535,7 @@ def cpu_baseline(method, seed, length, offsets_host, got, budget_s, samples, seg
         hoff = np.zeros(n + 1, dtype=np.uint64)
         np.cumsum(np.uint64(4) + xlens[:n].astype(np.uint64), out=hoff[1:])
         runv = lambda k, v, th: O.batch_offsets(method, host, hoff[:k + 1], variant=v, nthreads=th)  # noqa: E731
+        prod = lambda th: product_batch(method, host, th, offsets=hoff)  # noqa: E731
         sample_bytes = int(offsets_host[n])
         what = (f"the first {n} messages ({sample_bytes} B): the hashed streams (host-order length + payload "
                 f"bytes) an XDR build feeds mchecksum_update")
@@ -535,6 +551,7 @@ def cpu_baseline(method, seed, length, offsets_host, got, budget_s, samples, seg
         n = min(4096 if length <= 65536 else 256, len(got))
         host = O.splitmix_bytes(n * length, seed)
         runv = lambda k, v, th: O.batch_fixed(method, host, length, length, k, variant=v, nthreads=th)  # noqa: E731
+        prod = lambda th: product_batch(method, host, th, count=n, length=length)  # noqa: E731
         sample_bytes = n * length
         what = f"{n} x {length} B"
     else:
@@ -542,6 +559,7 @@ def cpu_baseline(method, seed, length, offsets_host, got, budget_s, samples, seg
         host = O.splitmix_bytes(int(offsets_host[n]), seed)
         sub = np.ascontiguousarray(offsets_host[:n + 1])
         runv = lambda k, v, th: O.batch_offsets(method, host, sub[:k + 1], variant=v, nthreads=th)  # noqa: E731
+        prod = lambda th: product_batch(method, host, th, offsets=sub)  # noqa: E731
         sample_bytes = int(offsets_host[n])
         what = f"the first {n} payloads ({sample_bytes} B) of the offsets layout"
     run = lambda k: runv(k, variant, threads)  # noqa: E731
@@ -577,6 +595,31 @@ def cpu_baseline(method, seed, length, offsets_host, got, budget_s, samples, seg
             if e2 >= budget_s / 3 or p2 >= 50:
                 break
         breakdown[f"{v}_{th}thread{'s' if th > 1 else ''}"] = round(p2 * sample_bytes / e2 / 2**30, 2)
+    # ... and the PRODUCT's own CPU path on the same sample (libmchecksum's
+    # streaming API, one object per thread: the AVX-512 VPCLMULQDQ fold for
+    # updates >= 1 KiB; tools/cpu_batch.c), at full width and on one thread --
+    # what the host can actually do, next to the oracle port above.  Its CRCs
+    # must equal the oracle's.
+    for th in (threads, 1):
+        key = f"product_{th}thread{'s' if th > 1 else ''}"
+        try:
+            pv = prod(th)
+        except OSError as e:  # build/libcpu_batch.so absent
+            breakdown[key] = None
+            base["product_note"] = f"product CPU path not timed: {e}"
+            break
+        if not np.array_equal(pv.astype(want.dtype), want):
+            breakdown[key] = None
+            base["product_note"] = "product CPU path disagrees with the oracle"
+            break
+        p2, t2 = 0, time.perf_counter()
+        while True:
+            prod(th)
+            p2 += 1
+            e2 = time.perf_counter() - t2
+            if e2 >= budget_s / 3 or p2 >= 200:
+                break
+        breakdown[key] = round(p2 * sample_bytes / e2 / 2**30, 2)
     base["breakdown_GiB_s"] = breakdown
     base["cpu_model"] = _cpu_model()
 
@@ -611,6 +654,37 @@ def cpu_baseline(method, seed, length, offsets_host, got, budget_s, samples, seg
     where = f" across all {world} shares" if world > 1 else ""
     parity = f"bit-exact ({checked} payloads{where} vs oracle)" if bad == 0 else f"MISMATCH {bad}/{checked}{where}"
     return base, parity
+
+
+_CPU_BATCH = None
+
+
+def product_batch(method, host, threads, count=None, length=None, offsets=None):
+    """CRCs (u64) of the product's CPU streaming path over a host batch:
+    fixed (count x length, packed) or an offsets table (build/libcpu_batch.so,
+    tools/cpu_batch.c, on `threads` pthreads)."""
+    import ctypes
+    global _CPU_BATCH
+    if _CPU_BATCH is None:
+        L = ctypes.CDLL(os.path.join(ROOT, "build", "libcpu_batch.so"))
+        vp, sz = ctypes.c_void_p, ctypes.c_size_t
+        L.cpu_batch_fixed.argtypes = [ctypes.c_char_p, vp, sz, sz, sz, vp, ctypes.c_int]
+        L.cpu_batch_offsets.argtypes = [ctypes.c_char_p, vp, vp, sz, vp, ctypes.c_int]
+        _CPU_BATCH = L
+    host = np.ascontiguousarray(host)
+    if offsets is not None:
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        count = len(offsets) - 1
+        out = np.zeros(count, dtype=np.uint64)
+        rc = _CPU_BATCH.cpu_batch_offsets(method.encode(), host.ctypes.data, offsets.ctypes.data, count,
+                                          out.ctypes.data, threads)
+    else:
+        out = np.zeros(count, dtype=np.uint64)
+        rc = _CPU_BATCH.cpu_batch_fixed(method.encode(), host.ctypes.data, length, length, count, out.ctypes.data,
+                                        threads)
+    if rc != 0:
+        raise RuntimeError(f"cpu_batch {method}: rc {rc}")
+    return out
 
 
 def xdr_offsets(seed, count):

@@ -27,17 +27,17 @@
  * Streams: `stream` is a hipStream_t (NULL = the default stream).  Calls are
  * asynchronous and capture-safe once mchecksum_gpu_prepare() has run for the
  * method on the current device (it uploads the lookup tables).  Large batches
- * balance their payloads through a device-side work-queue slot of their
- * stream's own (launches on one stream never overlap; host threads may share
- * a stream -- each launch takes the slot's launch lock while it is enqueued).
- * (A handle names a new stream only after hipStreamDestroy of the old one,
- * which returns once that stream's work has completed, so a reused handle
- * never shares its slot with launches in flight.)  A device has 2048 slots; once all are owned,
- * a new stream takes over the least recently used slot whose launches have
- * all completed.  Calls captured into a hipGraph, calls on hipStreamPerThread
- * and streams that find no idle slot take a plain static split of the batch
- * instead: a graph replays its captured arguments, possibly on two execs at
- * once, so no slot could be exclusive to it.
+ * balance their payloads through a device-side work-queue slot: each launch
+ * takes an idle one of the device's 2048 slots and holds it until it
+ * completes (a HIP event recorded by the launch's completion, queried without
+ * blocking), so no slot ever serves two launches at once -- whatever the
+ * streams, host threads, stream handle reuse or hipStreamDestroy timing.
+ * Calls captured into a hipGraph, and calls that find the oldest in-flight
+ * slots all still busy with no idle one left, take a plain static split of
+ * the batch instead: a graph replays its captured arguments, possibly on two
+ * execs at once, so no slot could be exclusive to it.  Destroying a stream
+ * with calls in flight follows the HIP rules for the memory those calls use;
+ * the library itself keeps no per-stream state.
  *
  * Fail closed: every wait in the work queue is bounded.  A launch in which a
  * wait gives up (a protocol fault; 0 in every test run) adds 1 to the error
@@ -238,14 +238,15 @@ mchecksum_gpu_queue_faults(void);
 /* Diagnostics: work-queue slot bookkeeping of the current device since the
  * library was loaded, written to stats[0 .. min(n, MCHECKSUM_GPU_QSTAT_COUNT)):
  * launches given a slot, launches that took the static split for want of one
- * (graph captures, hipStreamPerThread, no idle slot), slots that changed
- * owner stream, busy slots passed over while looking for one, and streams
- * that currently own a slot.  Host-side counters only: no device sync. */
+ * (graph captures, no idle slot), slots returned to the idle pool once their
+ * launch had completed, busy in-flight slots looked at while reaping, and
+ * slots handed out and not yet reaped.  Host-side counters only: no device
+ * sync. */
 #define MCHECKSUM_GPU_QSTAT_SLOT 0
 #define MCHECKSUM_GPU_QSTAT_NOSLOT 1
-#define MCHECKSUM_GPU_QSTAT_RECLAIM 2
+#define MCHECKSUM_GPU_QSTAT_REAPED 2
 #define MCHECKSUM_GPU_QSTAT_BUSY_SKIP 3
-#define MCHECKSUM_GPU_QSTAT_OWNERS 4
+#define MCHECKSUM_GPU_QSTAT_IN_FLIGHT 4
 #define MCHECKSUM_GPU_QSTAT_COUNT 5
 MCHECKSUM_PUBLIC int
 mchecksum_gpu_queue_stats(long long *stats, size_t n);

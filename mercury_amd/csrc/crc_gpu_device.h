@@ -212,14 +212,15 @@ constexpr uint64_t kSplitBytes = 256u << 10;
 // instead had the launch's last group zero its own bank at exit, behind a
 // hierarchical exit count (LDS per workgroup, a line per group, one per
 // slot): three dependent device-scope atomics, the zeroing and a wait after
-// the last wave's last payload, on every launch's critical path.  Now a
-// workgroup's exit is one non-returning add on its group's completion line.
+// the last wave's last payload, on every launch's critical path.  Round 3
+// kept one non-returning add per workgroup on a completion line, summed by the
+// host (a device round trip) before it gave a slot to another stream; round 4
+// records a HIP event at each slot launch's completion instead
+// (hipExtLaunchKernel's stop event, queried without blocking, queue_slot), so
+// a workgroup's exit touches no slot line.
 // Bank layout (one counter per 256-B line, 8 KiB per bank, 16 KiB-aligned
 // slots): [0, 8) sub-queue tickets, [8] fault flag of the launch -- both
-// zeroed by the previous launch on the slot -- and [9, 17) completed
-// workgroups per group (blockIdx % 8; never zeroed: the host sums both
-// banks' and compares with the workgroups it issued before it gives the slot
-// to another stream, queue_slot).
+// zeroed by the previous launch on the slot.
 //
 // Exclusivity.  A slot serves one launch at a time: the host hands the queue
 // only to eager launches, each on a slot of its stream's own (launches on one
@@ -236,12 +237,12 @@ constexpr uint64_t kSplitBytes = 256u << 10;
 constexpr uint32_t kQSub = 8;
 constexpr uint32_t kQStride = 32;  // u64 words between counters
 constexpr uint32_t kQFault = kQSub;
-constexpr uint32_t kQBankLines = kQSub + 1;  // protocol lines, zeroed before the bank's next use
-constexpr uint32_t kQDone = kQBankLines;     // [kQDone, kQDone + kQSub): completed workgroups per group
+constexpr uint32_t kQMask = kQSub + 1;       // drained sub-queues (bit k), MCK_QMASK
+constexpr uint32_t kQBankLines = kQSub + 2;  // protocol lines, zeroed before the bank's next use
 constexpr uint64_t kQBankBytes = 8192;
 constexpr uint32_t kQBankWords = (uint32_t)(kQBankBytes / 8);
 constexpr uint32_t kQSlotWords = 2 * kQBankWords;  // slots 2 * kQBankBytes aligned: bank ^ kQBankBytes = the other
-static_assert((kQDone + kQSub) * kQStride <= kQBankWords, "bank overflow");
+static_assert(kQBankLines * kQStride <= kQBankWords, "bank overflow");
 // Chunk size: a power of two, about a quarter of a workgroup's fair share
 // of units, between 1 and 32 (C4: 32 units; a 5000-payload batch: 4).
 // Fixed 16 starved half the workgroups of C3's 8192 units at 2 WGs per CU; 32
@@ -305,7 +306,6 @@ constexpr uint64_t kNoChunk = 0xFFFFFFFFull;
 struct WgQueue {
     unsigned int slot;     // next (chunk, unit) slot of this workgroup
     unsigned int drained;  // sub-queues (counted from home) found empty
-    unsigned int exited;   // waves of this workgroup that left the loop
     unsigned int busy;     // 1: no slot for this launch -> static split
     unsigned int reads[kWgRing];
     unsigned long long entry[kWgRing];  // (chunk seq << 32) | global chunk id
@@ -369,10 +369,21 @@ constexpr uint32_t kSpinMax = 1u << 24;
 #ifndef MCK_STEAL_ROT
 #define MCK_STEAL_ROT 1
 #endif
+// Drained-state broadcast (round 4, A/B knob): a workgroup that finds
+// sub-queue k exhausted sets bit k of the bank's mask line; a thief reads the
+// mask once per fetch and skips the sub-queues already known drained instead
+// of spending a returning device atomic on each.
+#ifndef MCK_QMASK
+#define MCK_QMASK 0
+#endif
 // One lane: the next global chunk id for this workgroup, or kNoChunk.
 __device__ uint64_t wg_fetch(WgQueue *L, unsigned long long *q, uint64_t nch) {
     const uint32_t home = blockIdx.x % kQSub;
     uint32_t d = lds_ld(&L->drained);
+#if MCK_QMASK
+    uint64_t mask = 0;
+    bool have_mask = false;
+#endif
     while (d < kQSub) {
 #if MCK_STEAL_ROT
         // thieves of one home start at different victims (a rotation of the
@@ -382,11 +393,22 @@ __device__ uint64_t wg_fetch(WgQueue *L, unsigned long long *q, uint64_t nch) {
 #else
         const uint32_t k = (home + d) % kQSub;
 #endif
+#if MCK_QMASK
+        if (d > 0 && !have_mask) {
+            mask = __hip_atomic_load(q + kQMask * kQStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            have_mask = true;
+        }
+        if (!((mask >> k) & 1ull)) {
+#endif
         // sub-queue k owns chunks k, k + 8, k + 16, ...: every XCD streams
         // from the same moving window of the batch (contiguous per-XCD ranges
         // -- 8 windows far apart -- measured 8% slower on the headline batch)
         const uint64_t t = atomicAdd(q + k * kQStride, 1ull);
         if (k + t * kQSub < nch) return k + t * kQSub;
+#if MCK_QMASK
+        if (!have_mask || !((mask >> k) & 1ull)) atomicOr(q + kQMask * kQStride, 1ull << k);
+        }
+#endif
         atomicMax(&L->drained, d + 1);
         const uint32_t seen = lds_ld(&L->drained);
         d = seen > d + 1 ? seen : d + 1;
@@ -430,7 +452,6 @@ __device__ bool wg_publish(WgQueue *L, uint32_t seq, uint64_t id, uint32_t cl) {
 __device__ __attribute__((unused)) void wg_queue_reset(WgQueue *L, unsigned long long *q) {
     L->slot = 0;
     L->drained = 0;
-    L->exited = 0;
     L->busy = q == nullptr;
     for (uint32_t r = 0; r < kWgRing; r++) {
         L->reads[r] = 0;
@@ -460,19 +481,6 @@ __device__ __forceinline__ T wave_max(T v) {
         v = o > v ? o : v;
     }
     return v;
-}
-
-// Exit of a launch that holds a slot, run by every wave once it has no more
-// units (wave-uniform): waves count in LDS (*wg_exited); the last wave of a
-// workgroup adds one, without waiting for the result, to its group's
-// completion line of the launch's bank (one add per workgroup, spread over 8
-// lines: one global add per wave on a single line serialised ~4096 x 45 ns
-// and ran C2 2x slower, round 1).
-__device__ __forceinline__ void slot_exit(unsigned long long *queue, uint32_t *wg_exited) {
-    const bool l0 = (threadIdx.x & 63u) == 0;
-    uint32_t wl = 0;
-    if (l0) wl = atomicAdd(wg_exited, 1u) == blockDim.x / 64u - 1u;
-    if (l0 && wl) atomicAdd(queue + (kQDone + blockIdx.x % kQSub) * kQStride, 1ull);
 }
 
 // Calls body(u) for this wave's units: through the work queue (DYN: the
@@ -610,11 +618,9 @@ __device__ __forceinline__ bool for_each_unit(WgQueue *L, unsigned long long *qu
         }
 #endif
         if (__builtin_amdgcn_readfirstlane(lds_ld(&L->busy))) return false;  // no slot
-        // The first faulting wave of the launch claims the bank's fault flag
-        // (before its own exit is counted, so the slot cannot be released yet).
+        // The first faulting wave of the launch claims the bank's fault flag.
         uint32_t first = 0;
         if (l0 && flt) first = atomicCAS(queue + kQFault * kQStride, 0ull, 1ull) == 0ull;
-        slot_exit(queue, &L->exited);
         (void)nw;
         return __builtin_amdgcn_readfirstlane(first) != 0;
     } else {

@@ -4,11 +4,14 @@
 #ifndef MCK_GPU_HOST_H
 #define MCK_GPU_HOST_H
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdint>
+#include <deque>
 #include <mutex>
-#include <unordered_map>
+#include <vector>
 
 #include "crc_gpu_device.h"
 #include "mchecksum_models.h"
@@ -21,13 +24,12 @@ constexpr uint32_t kStreamSlots = 2048;
 constexpr uint32_t kQueueSlots = kStreamSlots;
 
 // One slot: the work-queue counters (kQSlotWords words in DevCtx::queue),
-// owned by one stream at a time.
+// held by one launch at a time, from queue_slot() until that launch's
+// completion.
 struct SlotState {
-    uintptr_t sid = 0;  // owning stream (handle)
-    uint64_t issued_wgs = 0;     // workgroups of the launches handed this slot (each counts its completion, kQDone)
-    uint64_t seq = 0;            // launches enqueued on the slot: launch s counts in bank s & 1 (guarded by its launch lock)
-    uint64_t last_use = 0;       // LRU tick
-    bool owned = false;
+    uint64_t seq = 0;            // launches enqueued on the slot: launch s counts in bank s & 1
+    hipEvent_t done = nullptr;   // recorded by the completion of the slot's latest launch (hipExtLaunchKernel stop event)
+    std::atomic<bool> pending{false};  // handed out, launch not yet enqueued (its event not yet recorded)
 };
 
 struct DevCtx {
@@ -36,40 +38,53 @@ struct DevCtx {
     void *pack[MCK_NMODELS][CRC_GPU_MAX_LOG2G + 1] = {};
     void *ext[MCK_NMODELS] = {};  // mchecksum_gpu_ext.hip's per-model tables
     // Work-queue slots of the batch kernels (WgQueue, crc_gpu_device.h):
-    // kQueueSlots zeroed counter sets of two banks each (crc_gpu_device.h):
-    // launch s on a slot uses bank s & 1 and zeroes the other for launch s + 1.
-    // Eager launches use a slot of their stream's own (keyed by the handle);
-    // launches on one stream never overlap.  When all slots are owned, the
-    // least recently used slot whose issued workgroups have all completed
-    // (kQDone) changes owner.
-    // Graph-captured launches, and streams that find no idle slot, get none
+    // kQueueSlots zeroed counter sets of two banks each: launch s on a slot
+    // uses bank s & 1 and zeroes the other for launch s + 1.  A slot serves one
+    // launch at a time: every eager queue launch takes an idle slot from the
+    // pool and holds it until its completion records the slot's `done` event
+    // (queried without blocking when the slot is reaped back into the pool).
+    // No stream owns a slot, so nothing depends on stream handles, their
+    // reuse after hipStreamDestroy, or host threads sharing a stream.
+    // Graph-captured launches, and launches that find no idle slot, get none
     // and take the plain static split (crc_gpu_device.h, "Exclusivity").
     unsigned long long *queue = nullptr;        // 2 * kQBankBytes-aligned view of queue_mem
     void *queue_mem = nullptr;
-    SlotState slot[kQueueSlots];               // guarded by g_mu
-    std::unordered_map<uintptr_t, uint32_t> sid_slot;  // guarded by g_mu
-    uint32_t nslots = 0;                        // slots handed out so far
-    uint64_t tick = 0;
-    hipStream_t probe = nullptr;                // private stream: reads kQDone words
-    unsigned long long *probe_host = nullptr;   // pinned copy of one slot for those reads
-    // Launch locks (slot i: launch_mu[i % kLaunchLocks]), held from the bank
-    // choice through the kernel's enqueue: two host threads launching on one
-    // stream then enqueue in bank order, so the device alternates the banks.
-    static constexpr uint32_t kLaunchLocks = 64;
-    std::mutex launch_mu[kLaunchLocks];
+    SlotState slot[kQueueSlots];
+    uint32_t nslots = kQueueSlots;              // slots in the pool (MCHECKSUM_GPU_QUEUE_SLOTS lowers it for tests)
+    std::vector<uint32_t> idle;                 // slots known idle; the most recently reaped on top (guarded by g_mu)
+    std::deque<uint32_t> in_flight;             // slots handed out, oldest first (guarded by g_mu)
     // diagnostics (mchecksum_gpu_queue_stats)
-    long long n_slot = 0, n_noslot = 0, n_reclaim = 0, n_busy_skip = 0;
+    long long n_slot = 0, n_noslot = 0, n_reaped = 0, n_busy_skip = 0;
 };
 
-// A launch's slot bank (counters), the slot's index and the launch's grid;
-// holds the slot's launch lock until the launch is enqueued (end of scope)
-// or taken back (slot_unissue).
+// A launch's slot bank (counters), the slot's index and its completion event.
+// The launch must record `done` (launch_kernel's `stop`) and then call
+// slot_issued(), or slot_unissue() if the launch call failed.
 struct SlotRef {
     unsigned long long *q = nullptr;
     int idx = -1;
-    uint32_t grid = 0;
-    std::unique_lock<std::mutex> lk;
+    hipEvent_t done = nullptr;
+    SlotState *st = nullptr;
 };
+
+// Enqueue kernel k on stream s and return THIS launch's status: hipLaunchKernel
+// / hipExtLaunchKernel report whether the launch was enqueued, where
+// hipGetLastError() would also return an earlier call's sticky error (and a
+// slot launch read as failed would be taken back while its kernel runs).
+// stop: an event the kernel's completion records (slot launches only; they are
+// never captured into graphs).  Arguments are converted to the kernel's
+// parameter types before their addresses are taken.
+template <class T>
+struct Param {
+    using type = T;
+};
+template <class... P>
+hipError_t launch_kernel(void (*k)(P...), dim3 grid, dim3 block, hipStream_t s, hipEvent_t stop,
+                         typename Param<P>::type... args) {
+    void *argv[] = {static_cast<void *>(&args)...};
+    if (stop) return hipExtLaunchKernel(reinterpret_cast<const void *>(k), grid, block, argv, 0, s, nullptr, stop, 0);
+    return hipLaunchKernel(reinterpret_cast<const void *>(k), grid, block, argv, 0, s);
+}
 
 extern std::mutex g_mu;
 
@@ -92,14 +107,13 @@ int prologue(const char *method, int log2g, int *width, DevCtx **c, const void *
 // Z^n shift pack of a 32/64-bit model, the byte table of a 16-bit one
 // (caller holds g_mu).
 int get_ext(DevCtx *c, int idx, const void **out);
-// Work-queue slot bank for one launch of `grid` workgroups of a throughput
-// (non-light) batch kernel on `stream`, exclusive to that stream; empty
-// (static split) for a launch being captured into a graph or a stream that
-// finds no idle slot.  Every workgroup of a launch given a slot must count
-// itself done on it (slot_exit): if the launch fails to start,
-// slot_unissue() takes the launch back.  Keep the SlotRef alive until the
-// kernel is enqueued: it holds the slot's launch lock.
-SlotRef queue_slot(DevCtx *c, void *stream, uint32_t grid);
+// Work-queue slot bank for one launch of a throughput (non-light) batch
+// kernel on `stream`, exclusive to that launch until it completes; empty
+// (static split) for a launch being captured into a graph or when no slot is
+// idle.  A launch given a slot passes r.done as launch_kernel's `stop` event,
+// then calls slot_issued() -- or slot_unissue() if the launch call failed.
+SlotRef queue_slot(DevCtx *c, void *stream);
+void slot_issued(SlotRef &r);
 void slot_unissue(DevCtx *c, SlotRef &r);
 // Queue-fault count of mchecksum_gpu_ext.hip's kernels (their own copy of
 // g_mck_queue_faults) on the current device; -1 on error.

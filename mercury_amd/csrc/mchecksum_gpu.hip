@@ -110,8 +110,8 @@ int swap_outputs(void *dev_out, uint64_t count, int width, void *stream) {
     if (!count) return MCHECKSUM_GPU_OK;
     uint64_t blocks = (count + 255) / 256;
     blocks = blocks > 1024 ? 1024 : blocks;
-    hipLaunchKernelGGL(bswap_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, dev_out, count, width);
-    hipError_t e = hipGetLastError();
+    const hipError_t e =
+        launch_kernel(bswap_kernel, dim3((unsigned)blocks), dim3(256), (hipStream_t)stream, nullptr, dev_out, count, width);
     if (e != hipSuccess) return hip_err(e, "output byte swap");
     return MCHECKSUM_GPU_OK;
 }
@@ -127,6 +127,12 @@ int device_ctx(DevCtx **out) {
         e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         if (e != hipSuccess) return hip_err(e, "hipDeviceGetAttribute");
         c.cus = cus > 0 ? cus : 1;
+        // tests only: a smaller slot pool (MCHECKSUM_GPU_QUEUE_SLOTS=n), so a
+        // test can hold every slot in flight
+        if (const char *env = getenv("MCHECKSUM_GPU_QUEUE_SLOTS")) {
+            const long v = atol(env);
+            if (v >= 1 && v < (long)kQueueSlots) c.nslots = (uint32_t)v;
+        }
         // slots aligned to two banks, so a bank's partner is its address ^ kQBankBytes
         const size_t slot_bytes = (size_t)kQSlotWords * sizeof(unsigned long long);
         const size_t qbytes = (size_t)kQueueSlots * slot_bytes + slot_bytes;
@@ -135,14 +141,10 @@ int device_ctx(DevCtx **out) {
         if (e == hipSuccess)
             c.queue = reinterpret_cast<unsigned long long *>((reinterpret_cast<uintptr_t>(c.queue_mem) + slot_bytes - 1) /
                                                              slot_bytes * slot_bytes);
-        if (e == hipSuccess) e = hipStreamCreateWithFlags(&c.probe, hipStreamNonBlocking);
-        if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&c.probe_host), slot_bytes);
         if (e != hipSuccess) {
             if (c.queue_mem) (void)hipFree(c.queue_mem);
-            if (c.probe) (void)hipStreamDestroy(c.probe);
             c.queue_mem = nullptr;
             c.queue = nullptr;
-            c.probe = nullptr;
             return hip_err(e, "work-queue allocation");
         }
         c.init = true;
@@ -188,117 +190,106 @@ int get_pack(DevCtx *c, int idx, int log2g, const void **pack) {
     return 0;
 }
 
-// Whether slot i has completed every workgroup it was issued (the kQDone
-// lines of both banks, read on the private stream); false if the read fails
-// (caller holds g_mu).
-bool slot_idle(DevCtx *c, uint32_t i) {
-    if (hipMemcpyAsync(c->probe_host, c->queue + (size_t)i * kQSlotWords, (size_t)kQSlotWords * sizeof(unsigned long long),
-                       hipMemcpyDeviceToHost, c->probe) != hipSuccess ||
-        hipStreamSynchronize(c->probe) != hipSuccess) {
-        (void)hipGetLastError();
-        return false;
-    }
-    uint64_t done = 0;
-    for (uint32_t b = 0; b < 2; b++)
-        for (uint32_t g = 0; g < kQSub; g++) done += c->probe_host[b * kQBankWords + (kQDone + g) * kQStride];
-    return done == c->slot[i].issued_wgs;
+// Whether slot s is idle: handed to no launch that has not yet been enqueued,
+// and its latest launch has completed -- its `done` event, recorded by that
+// launch's completion (launch_kernel's stop event), queried without blocking:
+// no device round trip, so it may run under g_mu.  A never-recorded event
+// reads as complete.
+bool slot_idle(const SlotState &s) {
+    if (s.pending.load(std::memory_order_acquire)) return false;
+    const hipError_t e = hipEventQuery(s.done);
+    if (e == hipSuccess) return true;
+    if (e != hipErrorNotReady) (void)hipGetLastError();
+    return false;
 }
 
-SlotRef queue_slot(DevCtx *c, void *stream, uint32_t grid) {
+// In-flight slots looked at per queue_slot call: a couple while the pool has
+// idle slots (so the most recently used lines, warm in L2, are reused first),
+// more when it is empty.
+constexpr uint32_t kReapSome = 2, kReapMax = 8;
+
+SlotRef queue_slot(DevCtx *c, void *stream) {
     SlotRef r;
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing((hipStream_t)stream, &st) != hipSuccess) {
         (void)hipGetLastError();
         st = hipStreamCaptureStatusNone;
     }
+    std::lock_guard<std::mutex> lk(g_mu);
     // A captured launch replays with these arguments, possibly on two graph
-    // execs at once: no exclusive slot exists for it, so it takes the static
+    // execs at once: no slot can be exclusive to it, so it takes the static
     // split (crc_gpu_device.h, "Exclusivity").
     if (st != hipStreamCaptureStatusNone) {
-        std::lock_guard<std::mutex> lk(g_mu);
         c->n_noslot++;
         return r;
     }
-    // hipStreamPerThread names a different stream in every host thread: one
-    // slot for that handle could serve two launches at once
-    std::unique_lock<std::mutex> lk(g_mu);
-    if ((hipStream_t)stream == hipStreamPerThread) {
+    if (c->idle.empty() && c->in_flight.empty())  // first use on this device: every slot idle, slot 0 on top
+        for (uint32_t k = c->nslots; k-- > 0;) c->idle.push_back(k);
+    // Reap: return the oldest in-flight slots whose launches have completed.
+    const uint32_t limit = c->idle.empty() ? kReapMax : kReapSome;
+    uint32_t looked = 0, busy = 0;
+    for (auto it = c->in_flight.begin(); it != c->in_flight.end() && looked < limit; looked++) {
+        if (slot_idle(c->slot[*it])) {
+            c->idle.push_back(*it);
+            it = c->in_flight.erase(it);
+            c->n_reaped++;
+        } else {
+            ++it;
+            busy++;
+        }
+    }
+    if (c->idle.empty()) {  // the oldest launches are all still running: static split
+        c->n_busy_skip += busy;
         c->n_noslot++;
         return r;
     }
-    // Keyed by handle.  A handle names a new stream only after the old one was
-    // destroyed, and hipStreamDestroy returns once the stream's queued work has
-    // completed (measured: tests/test_gpu_queue.py, destroy with a launch in
-    // flight), so the new owner never overlaps the old owner's launches.
-    const uintptr_t sid = reinterpret_cast<uintptr_t>(stream);
-    uint32_t i;
-    auto it = c->sid_slot.find(sid);
-    if (it != c->sid_slot.end()) {
-        i = it->second;  // this stream's own slot: its launches never overlap
-    } else if (c->nslots < kQueueSlots) {
-        i = c->nslots++;
-    } else {
-        // All slots owned: the least recently used ones, oldest first, until
-        // one has completed every launch it was issued (a destroyed stream's
-        // work may still be in flight).  None idle among the oldest 8: this
-        // launch takes the static split.
-        uint32_t cand[8];
-        uint64_t ct[8];
-        uint32_t nc = 0;
-        for (uint32_t k = 0; k < kQueueSlots; k++) {
-            const uint64_t t = c->slot[k].last_use;
-            uint32_t pos = nc < 8 ? nc++ : 8;
-            if (pos == 8) {
-                if (t >= ct[7]) continue;
-                pos = 7;
-            }
-            while (pos > 0 && ct[pos - 1] > t) {
-                ct[pos] = ct[pos - 1];
-                cand[pos] = cand[pos - 1];
-                pos--;
-            }
-            ct[pos] = t;
-            cand[pos] = k;
-        }
-        i = kQueueSlots;
-        for (uint32_t k = 0; k < nc && i == kQueueSlots; k++) {
-            if (slot_idle(c, cand[k])) i = cand[k];
-            else c->n_busy_skip++;
-        }
-        if (i == kQueueSlots) {
-            c->n_noslot++;
-            return r;
-        }
-        c->sid_slot.erase(c->slot[i].sid);
-        c->n_reclaim++;
-    }
+    const uint32_t i = c->idle.back();
     SlotState &s = c->slot[i];
-    if (!s.owned || s.sid != sid) {
-        s.owned = true;
-        s.sid = sid;
-        c->sid_slot[sid] = i;
+    if (!s.done && hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess) {
+        (void)hipGetLastError();
+        s.done = nullptr;
+        c->n_noslot++;
+        return r;
     }
-    s.issued_wgs += grid;  // busy from here on: no other stream can reclaim it
-    s.last_use = ++c->tick;
+    c->idle.pop_back();
+    c->in_flight.push_back(i);
+    c->n_busy_skip += busy;
     c->n_slot++;
-    lk.unlock();
-    // The bank is chosen under the slot's launch lock, held until the caller
-    // has enqueued the kernel: launches of several host threads on one stream
-    // reach the device in the order of their banks.
-    r.lk = std::unique_lock<std::mutex>(c->launch_mu[i % DevCtx::kLaunchLocks]);
+    s.pending.store(true, std::memory_order_relaxed);
     r.q = c->queue + (size_t)i * kQSlotWords + (s.seq & 1u) * kQBankWords;
     s.seq++;
     r.idx = (int)i;
-    r.grid = grid;
+    r.done = s.done;
+    r.st = &s;
     return r;
 }
 
+// The launch holding r is enqueued and its completion event recorded: the
+// slot now reads busy until that launch completes.
+void slot_issued(SlotRef &r) {
+    if (r.st) r.st->pending.store(false, std::memory_order_release);
+}
+
+// The launch call failed, so the kernel was not enqueued (launch_kernel
+// reports the call's own status): the bank it was given is still clean, and
+// the slot goes straight back to the pool.
 void slot_unissue(DevCtx *c, SlotRef &r) {
     if (r.idx < 0) return;
-    c->slot[r.idx].seq--;  // under the launch lock r still holds
-    r.lk.unlock();
     std::lock_guard<std::mutex> lk(g_mu);
-    c->slot[r.idx].issued_wgs -= r.grid;
+    SlotState &s = c->slot[r.idx];
+    s.seq--;
+    for (auto it = c->in_flight.end(); it != c->in_flight.begin();) {
+        if (*--it == (uint32_t)r.idx) {
+            c->in_flight.erase(it);
+            break;
+        }
+    }
+    c->idle.push_back((uint32_t)r.idx);
+    c->n_slot--;
+    c->n_noslot++;
+    s.pending.store(false, std::memory_order_release);
+    r.idx = -1;
+    r.st = nullptr;
 }
 
 uint32_t *error_word() { return t_err_word; }
@@ -389,10 +380,15 @@ bool use_nt(uint64_t batch_bytes) {
     return batch_bytes >= (512ull << 20);
 }
 
-int launch(const KLaunch &kl, const BatchArgs &a, unsigned blocks, void *stream) {
-    hipLaunchKernelGGL(kl.k, dim3(blocks), dim3(kl.block), 0, (hipStream_t)stream, a);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return hip_err(e, "kernel launch");
+// Launch a batch kernel; a slot launch records the slot's completion event.
+// A failed launch call is taken back from its slot (slot_unissue).
+int launch(DevCtx *c, const KLaunch &kl, const BatchArgs &a, unsigned blocks, void *stream, SlotRef &sr) {
+    const hipError_t e = launch_kernel(kl.k, dim3(blocks), dim3(kl.block), (hipStream_t)stream, sr.done, a);
+    if (e != hipSuccess) {
+        slot_unissue(c, sr);
+        return hip_err(e, "kernel launch");
+    }
+    slot_issued(sr);
     return MCHECKSUM_GPU_OK;
 }
 
@@ -468,10 +464,9 @@ int do_offsets(const char *method, const void *base, const uint64_t *offsets, si
                    : (nt ? kernel_ptr<64, 6, kOffsets, false, true>() : kernel_ptr<64, 6, kOffsets, false>());
     SlotRef sr;
     const unsigned grid = grid_for(c, count, k);
-    if (dyn_policy(width, kOffsets, nt, light)) sr = queue_slot(c, stream, grid);
+    if (dyn_policy(width, kOffsets, nt, light)) sr = queue_slot(c, stream);
     a.queue = sr.q;
-    rc = launch(k, a, grid, stream);
-    if (rc != MCHECKSUM_GPU_OK) slot_unissue(c, sr);
+    rc = launch(c, k, a, grid, stream, sr);
     if (rc == MCHECKSUM_GPU_OK && gpu_msb(midx) && !verify) rc = swap_outputs(out, count, width, stream);
     return rc;
 }
@@ -525,19 +520,17 @@ int launch_fixed(DevCtx *c, int idx, const void *pack, int width, int lg, const 
         // in a half-zeroed output: tests/test_gpu_queue.py, concurrent replays)
         uint64_t zb = (count + 255) / 256;
         zb = zb > 1024 ? 1024 : zb;
-        hipLaunchKernelGGL(zero_u64_kernel, dim3((unsigned)zb), dim3(256), 0, (hipStream_t)stream,
-                           reinterpret_cast<unsigned long long *>(dev_out), (uint64_t)count);
-        hipError_t e = hipGetLastError();
+        const hipError_t e = launch_kernel(zero_u64_kernel, dim3((unsigned)zb), dim3(256), (hipStream_t)stream, nullptr,
+                                           reinterpret_cast<unsigned long long *>(dev_out), (uint64_t)count);
         if (e != hipSuccess) return hip_err(e, "output zeroing");
         const KLaunch k = nt ? KLaunch{crc64_batch_kernel<6, kFixedAligned, false, true, true>, Shape<64, kFixedAligned>::block,
                                        Shape<64, kFixedAligned>::blocks_per_cu}
                              : KLaunch{crc64_batch_kernel<6, kFixedAligned, false, false, true>, Shape<64, kFixedAligned>::block,
                                        Shape<64, kFixedAligned>::blocks_per_cu};
         const unsigned grid = grid_for(c, (uint64_t)count << sl, k);
-        SlotRef sr = queue_slot(c, stream, grid);
+        SlotRef sr = queue_slot(c, stream);
         a.queue = sr.q;
-        int rc = launch(k, a, grid, stream);
-        if (rc != MCHECKSUM_GPU_OK) slot_unissue(c, sr);
+        int rc = launch(c, k, a, grid, stream, sr);
         if (rc == MCHECKSUM_GPU_OK && gpu_msb(idx)) rc = swap_outputs(dev_out, count, width, stream);
         return rc;
     }
@@ -553,11 +546,10 @@ int launch_fixed(DevCtx *c, int idx, const void *pack, int width, int lg, const 
         blocks = (unsigned)(units < (uint64_t)c->cus ? (units ? units : 1) : c->cus);
     SlotRef sr;
     if (dyn) {
-        sr = queue_slot(c, stream, blocks);
+        sr = queue_slot(c, stream);
         a.queue = sr.q;
     }
-    int rc = launch(k, a, blocks, stream);
-    if (rc != MCHECKSUM_GPU_OK) slot_unissue(c, sr);
+    int rc = launch(c, k, a, blocks, stream, sr);
     if (rc == MCHECKSUM_GPU_OK && gpu_msb(idx)) rc = swap_outputs(dev_out, count, width, stream);
     return rc;
 }
@@ -689,8 +681,8 @@ int mchecksum_gpu_queue_stats(long long *stats, size_t n) {
     DevCtx *c = nullptr;
     int rc = device_ctx(&c);
     if (rc) return rc;
-    const long long v[MCHECKSUM_GPU_QSTAT_COUNT] = {c->n_slot, c->n_noslot, c->n_reclaim, c->n_busy_skip,
-                                                    (long long)c->sid_slot.size()};
+    const long long v[MCHECKSUM_GPU_QSTAT_COUNT] = {c->n_slot, c->n_noslot, c->n_reaped, c->n_busy_skip,
+                                                    (long long)c->in_flight.size()};
     for (size_t i = 0; i < n && i < MCHECKSUM_GPU_QSTAT_COUNT; i++) stats[i] = v[i];
     return MCHECKSUM_GPU_OK;
 }

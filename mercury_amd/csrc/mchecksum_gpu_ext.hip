@@ -844,43 +844,42 @@ int mchecksum_gpu_checksum_segments(const char *hash_method, const uint64_t *dev
     uint64_t zgrid = (out_words + kScanThreads - 1) / kScanThreads;
     zgrid = zgrid > 1024 ? 1024 : zgrid;
     const unsigned rgrid = (unsigned)(nb > zgrid ? nb : zgrid > 0 ? zgrid : 1);
-    hipLaunchKernelGGL(seg_scan_reduce, dim3(rgrid), dim3(kScanThreads), 0, s, dev_seg_len, dev_seg_addr,
-                       (uint64_t)nseg, nb, tot, (uint32_t *)dev_out, out_words);
+    hipError_t e = launch_kernel(seg_scan_reduce, dim3(rgrid), dim3(kScanThreads), s, nullptr, dev_seg_len, dev_seg_addr,
+                                 (uint64_t)nseg, nb, tot, (uint32_t *)dev_out, out_words);
     uint64_t *obj_w = width == 64 && MCK_SEG_QUEUE ? (uint64_t *)a.obj : nullptr;
     const char *scan3 = getenv("MCHECKSUM_GPU_SEG_SCAN3");  // tests: force the three-launch scan
-    if (nb >= 1 && nb <= kScanFusedBlocks && !(scan3 && scan3[0] == '1')) {
-        hipLaunchKernelGGL(seg_scan_down<true>, dim3((unsigned)nb), dim3(kScanThreads), 0, s, dev_seg_len,
-                           (uint64_t)nseg, (const uint64_t *)tot, nb, (uint64_t *)a.P, (uint64_t *)a.C,
-                           (unsigned long long *)a.ragged, dev_obj_first, (uint64_t)nobj, obj_w, (uint32_t *)a.map,
-                           a.map_cap);
+    if (e != hipSuccess) {
+    } else if (nb >= 1 && nb <= kScanFusedBlocks && !(scan3 && scan3[0] == '1')) {
+        e = launch_kernel(seg_scan_down<true>, dim3((unsigned)nb), dim3(kScanThreads), s, nullptr, dev_seg_len,
+                          (uint64_t)nseg, (const uint64_t *)tot, nb, (uint64_t *)a.P, (uint64_t *)a.C,
+                          (unsigned long long *)a.ragged, dev_obj_first, (uint64_t)nobj, obj_w, (uint32_t *)a.map,
+                          a.map_cap);
     } else {
-        hipLaunchKernelGGL(seg_scan_top, dim3(1), dim3(kScanThreads), 0, s, tot, nb, (uint64_t)nseg, (uint64_t *)a.P,
-                           (uint64_t *)a.C, (unsigned long long *)a.ragged);
-        if (nb)
-            hipLaunchKernelGGL(seg_scan_down<false>, dim3((unsigned)nb), dim3(kScanThreads), 0, s, dev_seg_len,
-                               (uint64_t)nseg, (const uint64_t *)tot, nb, (uint64_t *)a.P, (uint64_t *)a.C,
-                               (unsigned long long *)a.ragged, dev_obj_first, (uint64_t)nobj, obj_w,
-                               (uint32_t *)a.map, a.map_cap);
+        e = launch_kernel(seg_scan_top, dim3(1), dim3(kScanThreads), s, nullptr, tot, nb,
+                          (uint64_t)nseg, (uint64_t *)a.P, (uint64_t *)a.C, (unsigned long long *)a.ragged);
+        if (e == hipSuccess && nb)
+            e = launch_kernel(seg_scan_down<false>, dim3((unsigned)nb), dim3(kScanThreads), s, nullptr, dev_seg_len,
+                              (uint64_t)nseg, (const uint64_t *)tot, nb, (uint64_t *)a.P, (uint64_t *)a.C,
+                              (unsigned long long *)a.ragged, dev_obj_first, (uint64_t)nobj, obj_w,
+                              (uint32_t *)a.map, a.map_cap);
     }
-    hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_err(e, "segment scan launch");
     if (width == 32) {
-        hipLaunchKernelGGL((seg_kernel<32, 0>), dim3(c->cus), dim3(1024), 0, s, a);
+        e = launch_kernel(seg_kernel<32, 0>, dim3(c->cus), dim3(1024), s, nullptr, a);
     } else {
         // the aligned chunk pass takes the work queue; the ragged pass never
         // touches the slot (a.queue is cleared for it)
-        SlotRef sr = MCK_SEG_QUEUE ? queue_slot(c, stream, 2u * (uint32_t)c->cus) : SlotRef{};
+        SlotRef sr = MCK_SEG_QUEUE ? queue_slot(c, stream) : SlotRef{};
         a.queue = sr.q;
-        hipLaunchKernelGGL((seg_kernel<64, 1>), dim3(2 * c->cus), dim3(1024), 0, s, a);
-        e = hipGetLastError();
+        e = launch_kernel(seg_kernel<64, 1>, dim3(2 * c->cus), dim3(1024), s, sr.done, a);
         if (e != hipSuccess) {
             slot_unissue(c, sr);
             return hip_err(e, "segment kernel launch");
         }
+        slot_issued(sr);
         a.queue = nullptr;
-        hipLaunchKernelGGL((seg_kernel<64, 2>), dim3(c->cus), dim3(1024), 0, s, a);
+        e = launch_kernel(seg_kernel<64, 2>, dim3(c->cus), dim3(1024), s, nullptr, a);
     }
-    e = hipGetLastError();
     if (e != hipSuccess) return hip_err(e, "segment kernel launch");
     // MSB-first model: the kernels' values are the CRCs byte-swapped (crc_gpu_layout.h)
     if (gpu_msb(mck_model_index(hash_method))) return swap_outputs(dev_out, nobj, width, stream);
@@ -924,8 +923,7 @@ int mchecksum_gpu_verify_core_headers(const char *hash_method, int kind, const v
     a.xorout = (uint32_t)m.xorout;
     uint64_t blocks = (count + 255) / 256;
     if (blocks > (uint64_t)c->cus * 8) blocks = (uint64_t)c->cus * 8;
-    hipLaunchKernelGGL(core_header_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
-    hipError_t e = hipGetLastError();
+    const hipError_t e = launch_kernel(core_header_kernel, dim3((unsigned)blocks), dim3(256), (hipStream_t)stream, nullptr, a);
     if (e != hipSuccess) return hip_err(e, "core header kernel launch");
     return MCHECKSUM_GPU_OK;
 }
@@ -992,23 +990,22 @@ int mchecksum_gpu_checksum_xdr(const char *hash_method, const mchecksum_xdr_fiel
         a.err_word = error_word();
         uint64_t blocks = (count + 15) / 16;
         if (blocks > (uint64_t)c->cus) blocks = (uint64_t)c->cus;
-        SlotRef sr = queue_slot(c, stream, (uint32_t)blocks);
+        SlotRef sr = queue_slot(c, stream);
         a.queue = sr.q;
         auto k = width == 32 ? (nt ? xdr_fast_kernel<32, true> : xdr_fast_kernel<32, false>)
                              : (nt ? xdr_fast_kernel<64, true> : xdr_fast_kernel<64, false>);
-        hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(1024), 0, (hipStream_t)stream, a);
-        hipError_t e = hipGetLastError();
+        const hipError_t e = launch_kernel(k, dim3((unsigned)blocks), dim3(1024), (hipStream_t)stream, sr.done, a);
         if (e != hipSuccess) {
             slot_unissue(c, sr);
             return hip_err(e, "XDR kernel launch");
         }
+        slot_issued(sr);
         return MCHECKSUM_GPU_OK;
     }
     uint64_t blocks = (count + 3) / 4;
     if (blocks > (uint64_t)c->cus * 8) blocks = (uint64_t)c->cus * 8;
-    if (width == 32) hipLaunchKernelGGL(xdr_kernel<32>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
-    else hipLaunchKernelGGL(xdr_kernel<64>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
-    hipError_t e = hipGetLastError();
+    const hipError_t e = launch_kernel(width == 32 ? xdr_kernel<32> : xdr_kernel<64>, dim3((unsigned)blocks), dim3(256),
+                                       (hipStream_t)stream, nullptr, a);
     if (e != hipSuccess) return hip_err(e, "XDR kernel launch");
     return MCHECKSUM_GPU_OK;
 }

@@ -79,13 +79,14 @@ def queue_faults() -> int:
     return int(_lib().mchecksum_gpu_queue_faults())
 
 
-QSTAT_KEYS = ("slot", "noslot", "reclaim", "busy_skip", "owners")
+QSTAT_KEYS = ("slot", "noslot", "reaped", "busy_skip", "in_flight")
 
 
 def queue_stats() -> dict:
     """Work-queue slot bookkeeping of the current device (mchecksum_gpu_queue_stats):
-    launches given a slot, launches without one, slot owner changes, busy slots
-    passed over, streams owning a slot."""
+    launches given a slot, launches without one (graph captures, no idle slot),
+    slots reaped back into the idle pool, busy in-flight slots looked at while
+    reaping, slots handed out and not yet reaped."""
     import ctypes
     buf = (ctypes.c_longlong * len(QSTAT_KEYS))()
     rc = _lib().mchecksum_gpu_queue_stats(buf, len(QSTAT_KEYS))
@@ -131,8 +132,8 @@ def checksum_fixed(method: str, data: torch.Tensor, length: int, count: int | No
         raise GpuChecksumError("stride smaller than length")
     if out is None:
         out = torch.empty(count, dtype=out_dtype(method), device=data.device)
-    elif out.numel() < count or out.dtype != out_dtype(method) or not out.is_cuda:
-        raise GpuChecksumError("out tensor has the wrong size, dtype or device")
+    elif out.numel() < count or out.dtype != out_dtype(method) or not out.is_cuda or not out.is_contiguous():
+        raise GpuChecksumError("out tensor has the wrong size, dtype or device, or is not contiguous")
     _same_device(data, out=out)
     with _on(data):
         rc = _lib().mchecksum_gpu_checksum_fixed(method.encode(), data.data_ptr(), stride, length, count,
@@ -168,8 +169,8 @@ def checksum_offsets(method: str, data: torch.Tensor, offsets: torch.Tensor, out
         raise GpuChecksumError("offsets needs at least one entry")
     if out is None:
         out = torch.empty(count, dtype=out_dtype(method), device=data.device)
-    elif out.numel() < count or out.dtype != out_dtype(method) or not out.is_cuda:
-        raise GpuChecksumError("out tensor has the wrong size, dtype or device")
+    elif out.numel() < count or out.dtype != out_dtype(method) or not out.is_cuda or not out.is_contiguous():
+        raise GpuChecksumError("out tensor has the wrong size, dtype or device, or is not contiguous")
     _same_device(data, offsets=offsets, out=out)
     with _on(data):
         rc = _lib().mchecksum_gpu_checksum_offsets(method.encode(), data.data_ptr(), offsets.data_ptr(), count,
@@ -267,8 +268,8 @@ class SegmentBatch:
     def checksum(self, method: str, out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
         if out is None:
             out = torch.empty(self.nobj, dtype=out_dtype(method), device=self.device)
-        elif out.numel() < self.nobj or out.dtype != out_dtype(method) or not out.is_cuda:
-            raise GpuChecksumError("out tensor has the wrong size, dtype or device")
+        elif out.numel() < self.nobj or out.dtype != out_dtype(method) or not out.is_cuda or not out.is_contiguous():
+            raise GpuChecksumError("out tensor has the wrong size, dtype or device, or is not contiguous")
         if out.device != self.device:
             raise GpuChecksumError(f"out must be on {self.device}")
         base, n = self.meta.data_ptr(), self.nseg
@@ -348,8 +349,9 @@ def checksum_xdr(method: str, data: torch.Tensor, msg_offsets: torch.Tensor, sch
     fields = (XdrField * max(1, len(schema)))(*[XdrField(int(k), int(z)) for k, z in schema])
     if out is None:
         out = torch.empty(max(count, 0), dtype=out_dtype(method), device=data.device)
-    elif out.numel() < count or out.dtype != out_dtype(method) or out.device != data.device:
-        raise GpuChecksumError("out tensor has the wrong size, dtype or device")
+    elif (out.numel() < count or out.dtype != out_dtype(method) or out.device != data.device
+          or not out.is_contiguous()):
+        raise GpuChecksumError("out tensor has the wrong size, dtype or device, or is not contiguous")
     st = torch.ones(max(count, 0), dtype=torch.uint8, device=data.device) if status else None
     with _on(data):
         rc = _lib().mchecksum_gpu_checksum_xdr(method.encode(), fields, len(schema), data.data_ptr(),

@@ -25,6 +25,9 @@ def _free_port():
 LAYOUTS = {
     # name: (bench config, method, global count, payload length, seed, layout)
     "fixed": ("c5", "crc32c", 96, 65536, 0x4D43310000000005, "fixed"),
+    # the default at every N: the headline's per-GPU batch (weak scaling),
+    # here 48 payloads per rank -- global count 96 over 2 ranks
+    "weak_fixed": ("metric", "crc32c", 96, 65536, 0x4D43310000000005, "fixed"),
     "offsets": ("c4", "crc32c", 300, None, 0x4D43310000000004, "offsets"),
     "messages": ("msgs", "crc32c", 300, None, 0x4D43310000000004, "messages"),
     "segments": ("seg", "crc64", 6, 1 << 20, 0x4D43310000000003, "segments"),
@@ -82,7 +85,7 @@ def _worker(name, corrupt, rank, world, port, q):
         args = SimpleNamespace(steps=3, warmup=1, cpu_seconds=0.05, parity_samples=16, no_cpu_baseline=False)
         payload_bytes = count * length if length else int(off[-1] - off[0])
         r = SimpleNamespace(
-            config=cfg, method=method, seed=seed, length=length, layout=layout, strong=layout != "segments",
+            config=cfg, method=method, seed=seed, length=length, layout=layout, strong=cfg in bench.STRONG,
             global_count=gc if layout != "segments" else gc * world, count=count, plan=plan,
             payload_bytes=payload_bytes, alg_bytes=payload_bytes + 4 * count, gib_s=1.0, wall_max=0.003,
             kern_ms_max=1.0, achieved=1.0, per_rank=[[0.003, 1.0]] * world, world=world, got=got, offsets_host=off,
@@ -112,11 +115,30 @@ def test_two_rank_line_has_baseline_oracle_parity_and_traffic(name):
     cb = res["cpu_baseline"]
     assert cb["kind"] == "port" and cb["unit"] == "GiB/s" and cb["value"] > 0 and cb["cores"] >= 1
     assert cb["sample"] and "breakdown_GiB_s" in cb
+    # the product's own CPU path (libmchecksum streaming API on the same
+    # sample, oracle-checked) beside the oracle port, at full width and 1 thread
+    bd = cb["breakdown_GiB_s"]
+    prod = {k: v for k, v in bd.items() if k.startswith("product_")}
+    assert f"product_{cb['cores']}thread{'s' if cb['cores'] > 1 else ''}" in prod and "product_1thread" in prod, bd
+    assert all(v and v > 0 for v in prod.values()), (bd, cb.get("product_note"))
     assert res["parity"].startswith("bit-exact (") and "across all 2 shares vs oracle" in res["parity"], res["parity"]
     assert res["n_gpus"] == 2 and res["world_size"] == 2 and len(res["per_rank"]) == 2
     roof = res["roofline"]
     assert roof["traffic"] is not None and "rank 0's share" in roof["traffic_source"], roof
-    assert res["scaling"] == ("weak" if name == "segments" else "strong")
+    assert res["scaling"] == ("weak" if name in ("segments", "weak_fixed") else "strong")
+
+
+def test_default_multi_gpu_line_is_the_per_gpu_headline():
+    """bench.py --gpus N defaults to the headline's 65536 x 64 KiB per rank at
+    every N (weak scaling), so the driver's 1/2/4/8 series is one per-GPU
+    workload: the 2-rank line names 48 payloads on rank 0 out of 96 in all."""
+    import bench
+    assert bench.CONFIGS["metric"][1:3] == (65536, 65536) and "metric" not in bench.STRONG
+    res = _run("weak_fixed")
+    assert res["scaling"] == "weak" and res["metric"].endswith("64K x 64 KiB payloads")
+    cfg = res["config"]
+    assert cfg["payloads_rank0"] == 48 and cfg["global_batch"] == 96 and cfg["bytes_rank0"] == 48 * 65536
+    assert "48 x 65536 B payloads per GPU (96 in all over 2 GPUs)" in cfg["workload"], cfg["workload"]
 
 
 @pytest.mark.parametrize("name", ["fixed", "messages"])

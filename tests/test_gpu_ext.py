@@ -53,15 +53,14 @@ def _want(oracle_mod, method, host, segs, first):
     return out
 
 
-@pytest.mark.parametrize("method", ["crc32c", "crc64", "crc64-ecma182"])
-@pytest.mark.parametrize("map_cap", [None, "0", "40"])
+# the chunk map serves the CRC-64 queue pass only: its caps are CRC-64 cases
+@pytest.mark.parametrize("method,map_cap", [("crc32c", None), ("crc64", None), ("crc64-ecma182", None),
+                                            ("crc64", "0"), ("crc64", "40")])
 def test_segments_random_objects(gpu, buf, oracle_mod, method, map_cap, monkeypatch):
     """map_cap: the CRC-64 queue pass finds each chunk's segment in the scan's
     chunk map; "0" forces the search over the chunk prefix sums, "40" a map
     too small for the list (searched too, after partial map writes)."""
     if map_cap is not None:
-        if method != "crc64":
-            pytest.skip("the chunk map serves the CRC-64 queue pass only")
         monkeypatch.setenv("MCHECKSUM_GPU_SEG_MAP_CAP", map_cap)
     rng = np.random.default_rng(77 if method == "crc32c" else 78)
     host = _host(buf)
@@ -71,14 +70,11 @@ def test_segments_random_objects(gpu, buf, oracle_mod, method, map_cap, monkeypa
     assert got.tolist() == _want(oracle_mod, method, host, segs, first)
 
 
-@pytest.mark.parametrize("method", ["crc32c", "crc64"])
-@pytest.mark.parametrize("map_cap", [None, "0"])
+@pytest.mark.parametrize("method,map_cap", [("crc32c", None), ("crc64", None), ("crc64", "0")])
 def test_segments_one_huge_segment_and_chunk_edges(gpu, buf, oracle_mod, method, map_cap, monkeypatch):
     """One 20 MiB segment (80 chunks) and objects whose segment lengths sit on
     and around the 256 KiB chunk size; map_cap "0": chunk -> segment by search."""
     if map_cap is not None:
-        if method == "crc32c":
-            pytest.skip("the chunk map serves the CRC-64 queue pass only")
         monkeypatch.setenv("MCHECKSUM_GPU_SEG_MAP_CAP", map_cap)
     host = _host(buf)
     big = [(3, 20 << 20)]

@@ -285,3 +285,20 @@ def test_msb_first_method_verify(gpu, oracle_mod):
     t[int(off[victim])] ^= 0x20
     st, bad = gpu.verify_offsets("crc64-ecma182", t, offs, exp)
     assert int(bad.item()) == 1 and np.nonzero(st.cpu().numpy())[0].tolist() == [victim]
+
+
+def test_strided_out_is_refused(gpu):
+    """the kernels write `count` contiguous values at
+    out.data_ptr(), so a strided out view is refused on every entry point
+    that takes one, before any launch."""
+    import torch
+    data = torch.zeros(8 * 4096 + 64, dtype=torch.uint8, device="cuda")
+    offs = torch.arange(0, 9 * 4096, 4096, dtype=torch.int64, device="cuda")
+    strided = torch.empty(16, dtype=torch.int32, device="cuda")[::2]
+    assert strided.numel() == 8 and not strided.is_contiguous()
+    with pytest.raises(gpu.GpuChecksumError, match="contiguous"):
+        gpu.checksum_fixed("crc32c", data, 4096, count=8, out=strided)
+    with pytest.raises(gpu.GpuChecksumError, match="contiguous"):
+        gpu.checksum_offsets("crc32c", data, offs, out=strided)
+    with pytest.raises(gpu.GpuChecksumError, match="contiguous"):
+        gpu.checksum_xdr("crc32c", data, offs, [(2, 0)], out=strided)

@@ -118,12 +118,11 @@ print("shared stream ok", G.queue_stats())
 
 
 def test_threads_sharing_one_stream_alternate_the_slot_banks(gpu):
-    """8 host threads launch 480 queue batches onto ONE stream at once: the
-    stream's slot alternates two banks (crc_gpu_device.h, "Two banks per
-    slot"), which is only sound if the launches reach the device in the order
-    their banks were handed out -- the slot's launch lock (queue_slot) holds
-    from the bank choice through the enqueue.  Every result is exact and no
-    queue wait gave up."""
+    """8 host threads launch 480 queue batches onto ONE stream at once: each
+    launch holds a slot of its own from the pool until it completes
+    (queue_slot), so no two of them -- queued back to back on the stream, or
+    racing on the host -- ever count in one slot's banks.  Every result is
+    exact and no queue wait gave up."""
     r = subprocess.run([sys.executable, "-c", SHARED, ROOT], capture_output=True, text=True, timeout=110,
                        env=dict(os.environ, MCHECKSUM_GPU_LIGHT="0"))
     assert r.returncode == 0 and "shared stream ok" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]

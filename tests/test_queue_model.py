@@ -4,7 +4,9 @@ of every wave's shared-memory steps.  Checks what the GPU relies on: every
 unit is processed exactly once, no wait can block forever, and every launch
 leaves the bank the slot's next launch counts in at zero (two banks per slot,
 round 3: launch s counts in bank s & 1 and its first workgroup zeroes the
-other), with one completion per workgroup counted.
+other).  The host learns that a slot's launch has completed from the HIP event
+its completion records (round 4; queue_slot in mchecksum_gpu.hip) -- here, from
+every wave of the launch having returned.
 
 Each wave is a generator that yields at every access to shared state (LDS or
 the global slot), so a seeded scheduler explores many orders of the same
@@ -13,8 +15,8 @@ per-thread stream, streams past the table: crc_gpu_device.h "Exclusivity")
 takes the static split and never touches any slot; the fail-closed fault flag
 is modelled too.  Fetch triggers, chunk sizes (chunk_log2, the
 quarter-size tail chunks of ChunkPlan), the
-round-robin sub-queues, the LDS ring recycling, the bank zeroing and the exit
-counting mirror the device code one to one.
+round-robin sub-queues, the LDS ring recycling and the bank zeroing mirror the
+device code one to one.
 """
 import random
 
@@ -35,7 +37,6 @@ class Bank:
     def __init__(self):
         self.sub = [0] * QSUB          # sub-queue tickets
         self.fault = 0                 # first faulting wave of the launch
-        self.done = [0] * QSUB         # completed workgroups per group (never zeroed)
 
     def zero(self):  # wg_queue_init, workgroup 0: the protocol lines only
         self.sub = [0] * QSUB
@@ -48,23 +49,18 @@ class Bank:
 class Slot:
     def __init__(self):
         self.banks = [Bank(), Bank()]
-        self.issued = 0       # launches handed this slot (host: SlotState::issued)
-        self.issued_wgs = 0   # their workgroups (host: SlotState::issued_wgs)
-
-    def completed_wgs(self):
-        return sum(sum(b.done) for b in self.banks)
+        self.issued = 0       # launches handed this slot (host: SlotState::seq)
 
     def clean(self):
-        """Ready for the next launch: the bank it will count in is zeroed and
-        every workgroup issued so far has counted itself done."""
-        return self.banks[self.issued & 1].clean() and self.completed_wgs() == self.issued_wgs
+        """Ready for the next launch (the previous one has completed): the bank
+        it will count in is zeroed."""
+        return self.banks[self.issued & 1].clean()
 
 
 class Lds:
     def __init__(self):
         self.slot = 0
         self.drained = 0
-        self.exited = 0
         self.reads = [0] * RING
         self.entry = [(0xFFFFFFFF, 0)] * RING
         self.busy = False
@@ -94,7 +90,6 @@ def run_launches(launches, seed, slot=None, max_steps=4_000_000):
         if not spec.get("no_slot"):  # queue_slot: bank issued & 1, then count the launch
             bank = (slot.banks[slot.issued & 1], slot.banks[(slot.issued & 1) ^ 1])
             slot.issued += 1
-            slot.issued_wgs += spec["grid"]
         gens += _launch(spec, bank, rnd, r)
     steps = 0
     while gens:
@@ -201,13 +196,6 @@ def _launch(spec, bank, rnd, res):
             cur.fault = 1
             yield
             res["first_faults"] += first
-        # slot_exit: the workgroup's last wave counts it done on its group's line
-        prev_ex = L.exited  # atomicAdd on LDS: the returned old value decides
-        L.exited += 1
-        yield
-        if prev_ex == waves_per_wg - 1:
-            cur.done[b % QSUB] += 1
-            yield
 
     def init(b):  # wg_queue_init (thread 0 of the workgroup, before the barrier)
         L = lds[b]
@@ -287,4 +275,4 @@ def test_fault_flag_is_cleared_before_its_bank_is_reused():
         r = run_launches([dict(n=900, grid=4, wpw=4)], seed, slot)[0]
         assert r["units"] == list(range(900)) and r["first_faults"] == 0
         assert slot.clean()
-    assert slot.banks[0].fault == 0 and slot.completed_wgs() == 16
+    assert slot.banks[0].fault == 0 and slot.issued == 4

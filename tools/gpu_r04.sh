@@ -1,0 +1,103 @@
+#!/bin/bash
+# Round-4 GPU passes.  PART selects one:
+#   tests  -- new slot / fail-closed tests first, then the whole -m gpu suite
+#   ab     -- in-process A/B (tools/ab_variants.py): AB_VARIANTS of build/variants
+#             (default: working tree "cur" vs last commit "prev") plus the
+#             env pseudo-variants in AB_ENV, on AB_CONFIGS
+#   bench  -- bench.py per CONFIGS into gpurun_out/r04/bench_<config>.json
+#   trace  -- rocprofv3 kernel-trace summaries of bench.py per CONFIGS
+#   xcd    -- per-XCD end time and shader clock (tools/xcd_clock.py, trace build)
+#   pmc    -- FETCH_SIZE / WRITE_SIZE passes per CONFIGS -> pmc_traffic_<config>.json
+#   probe  -- tools/stream_probe (stream ids vs handles, completion-evidence cost)
+#   nccl   -- torchrun --nproc-per-node 1 bench.py (RCCL process group at world 1) per CONFIGS
+#   newtests -- TESTS (space-separated test files) only
+# Every GPU step has its own time limit; the first failure ends the script.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-/root/repo}
+cd "$R"; mkdir -p gpurun_out/r04
+O="$R/gpurun_out/r04"
+step() { echo "== $1 $(date +%T)"; }
+for P in ${PART:-tests}; do
+if [ "$P" = probe ]; then
+  step "stream probe"
+  timeout -k 10 120 ./build/stream_probe > $O/stream_probe.log 2>&1; rc=$?
+  cat $O/stream_probe.log; [ $rc -eq 0 ] || exit $rc
+fi
+if [ "$P" = newtests ]; then
+  step "tests $TESTS"
+  timeout -k 10 900 python -u -m pytest $TESTS -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_${TAG:-new}.log 2>&1; rc=$?
+  tail -15 $O/pytest_${TAG:-new}.log
+  [ $rc -eq 0 ] || { grep -E "Error|assert|FAILED|^E " $O/pytest_${TAG:-new}.log | head -60; exit $rc; }
+fi
+if [ "$P" = nccl ]; then
+  for c in ${CONFIGS:-c5}; do
+    step "torchrun 1 rank nccl $c"
+    timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node=1 --master-addr 127.0.0.1 --master-port 29533 \
+      bench.py --gpus 1 --config $c ${BENCH_ARGS:-} > $O/bench_nccl_1rank_$c.json 2> $O/bench_nccl_1rank_$c.err || { tail -30 $O/bench_nccl_1rank_$c.err; exit 1; }
+    cat $O/bench_nccl_1rank_$c.json
+  done
+fi
+if [ "$P" = tests ]; then
+  step "new tests"
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_slots.py tests/test_gpu_fail_closed.py -m gpu -x -v --timeout 300 \
+    --timeout-method thread > $O/pytest_new.log 2>&1; rc=$?
+  tail -15 $O/pytest_new.log
+  [ $rc -eq 0 ] || { grep -E "Error|assert|FAILED|^E " $O/pytest_new.log | head -60; exit $rc; }
+  step "full suite"
+  timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+    > $O/pytest_gpu.log 2>&1; rc=$?
+  tail -5 $O/pytest_gpu.log
+  [ $rc -eq 0 ] || { grep -E "Error|assert|FAILED|^E " $O/pytest_gpu.log | head -60; exit $rc; }
+fi
+if [ "$P" = ab ]; then
+  step "ab ${AB_CONFIGS:-c2,metric}"
+  timeout -k 10 600 python tools/ab_variants.py --config ${AB_CONFIGS:-c2,metric} --variants ${AB_VARIANTS:-prev cur} \
+    ${AB_ENV:-} --rounds ${AB_ROUNDS:-6} --iters ${AB_ITERS:-10} \
+    --out $O/ab_${AB_TAG:-r04}.json > $O/ab_${AB_TAG:-r04}.log 2>&1; rc=$?
+  grep -v amdgpu.ids $O/ab_${AB_TAG:-r04}.log; [ $rc -eq 0 ] || exit $rc
+fi
+if [ "$P" = xdrtest ]; then
+  step "xdr tests"
+  timeout -k 10 600 python -u -m pytest tests/test_xdr.py -m gpu -x -v --timeout 300 --timeout-method thread \
+    > $O/pytest_xdr.log 2>&1; rc=$?
+  tail -5 $O/pytest_xdr.log
+  [ $rc -eq 0 ] || { grep -E "Error|assert|FAILED|^E " $O/pytest_xdr.log | head -60; exit $rc; }
+fi
+if [ "$P" = bench ]; then
+  for c in ${CONFIGS:-metric c2}; do
+    step "bench $c"
+    timeout -k 10 300 python bench.py --config $c ${BENCH_ARGS:-} > $O/bench_$c.json 2> $O/bench_$c.err || { tail -20 $O/bench_$c.err; exit 1; }
+    cat $O/bench_$c.json
+  done
+fi
+if [ "$P" = driver ]; then
+  step "bench driver-style"
+  timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_driver.json 2> $O/bench_driver.err || { tail -20 $O/bench_driver.err; exit 1; }
+  cat $O/bench_driver.json
+fi
+if [ "$P" = xcd ]; then
+  step "xcd clock ${XCD_CONFIGS:-c2}"
+  timeout -k 10 300 python tools/xcd_clock.py ${XCD_CONFIGS:-c2} --out $O/xcd_clock.json > $O/xcd_clock.log 2>&1; rc=$?
+  grep -v amdgpu.ids $O/xcd_clock.log | tail -25; [ $rc -eq 0 ] || exit $rc
+fi
+if [ "$P" = trace ]; then
+  cd /tmp && export TMPDIR=/tmp
+  for c in ${CONFIGS:-c2}; do
+    step "kernel trace $c"
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$c -o bench -- python3 $R/bench.py --config $c ${BENCH_ARGS:-} > $O/prof_bench_$c.json 2> $O/prof_bench_$c.err || { tail $O/prof_bench_$c.err; exit 1; }
+    cat $O/prof_bench_$c.json
+  done
+  cd "$R"
+fi
+if [ "$P" = pmc ]; then
+  cd /tmp && export TMPDIR=/tmp
+  for c in ${CONFIGS:-c4}; do
+    step "pmc $c"
+    timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/tr_${c}_f -o p -- python3 $R/tools/kernel_run.py --config $c --iters 4 > $O/tr_${c}_f.log 2>&1 || { tail $O/tr_${c}_f.log; exit 1; }
+    timeout -k 10 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/tr_${c}_w -o p -- python3 $R/tools/kernel_run.py --config $c --iters 4 > $O/tr_${c}_w.log 2>&1 || { tail $O/tr_${c}_w.log; exit 1; }
+    k=batch_kernel; [ "$c" = xdr ] && k=xdr_fast_kernel
+    python3 $R/tools/pmc_traffic.py $O/tr_${c}_f $O/tr_${c}_w $k $O/pmc_traffic_$c.json $(python3 $R/tools/alg_bytes.py $c) 1 4 || exit 1
+  done
+  cd "$R"
+fi
+done
