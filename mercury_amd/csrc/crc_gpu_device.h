@@ -237,8 +237,7 @@ constexpr uint64_t kSplitBytes = 256u << 10;
 constexpr uint32_t kQSub = 8;
 constexpr uint32_t kQStride = 32;  // u64 words between counters
 constexpr uint32_t kQFault = kQSub;
-constexpr uint32_t kQMask = kQSub + 1;       // drained sub-queues (bit k), MCK_QMASK
-constexpr uint32_t kQBankLines = kQSub + 2;  // protocol lines, zeroed before the bank's next use
+constexpr uint32_t kQBankLines = kQSub + 1;  // protocol lines, zeroed before the bank's next use
 constexpr uint64_t kQBankBytes = 8192;
 constexpr uint32_t kQBankWords = (uint32_t)(kQBankBytes / 8);
 constexpr uint32_t kQSlotWords = 2 * kQBankWords;  // slots 2 * kQBankBytes aligned: bank ^ kQBankBytes = the other
@@ -366,24 +365,21 @@ constexpr uint32_t kSpinMax = 1u << 24;
         break;                            \
     }
 
+// Steal order (MCK_STEAL_ROT=0: every thief starts at home + 1).  On since
+// round 3: never slower in four one-process A/Bs over rounds 3-4 (headline
+// +0.1 to +0.2%, C4 +0.14 to +0.55%; profiles/r03/ab_steal_rot*.log,
+// profiles/r04/ab_qmask.log) -- gains inside the run-to-run band, kept because
+// the rotation is free (one index formula, a bijection over the other seven
+// sub-queues, run by the CPU model in tests/test_queue_model.py).  A drained-
+// state mask read before stealing (one load per fetch instead of an atomic on
+// each drained sub-queue) measured -0.1% / -0.5% and is gone.
 #ifndef MCK_STEAL_ROT
 #define MCK_STEAL_ROT 1
-#endif
-// Drained-state broadcast (round 4, A/B knob): a workgroup that finds
-// sub-queue k exhausted sets bit k of the bank's mask line; a thief reads the
-// mask once per fetch and skips the sub-queues already known drained instead
-// of spending a returning device atomic on each.
-#ifndef MCK_QMASK
-#define MCK_QMASK 0
 #endif
 // One lane: the next global chunk id for this workgroup, or kNoChunk.
 __device__ uint64_t wg_fetch(WgQueue *L, unsigned long long *q, uint64_t nch) {
     const uint32_t home = blockIdx.x % kQSub;
     uint32_t d = lds_ld(&L->drained);
-#if MCK_QMASK
-    uint64_t mask = 0;
-    bool have_mask = false;
-#endif
     while (d < kQSub) {
 #if MCK_STEAL_ROT
         // thieves of one home start at different victims (a rotation of the
@@ -393,22 +389,11 @@ __device__ uint64_t wg_fetch(WgQueue *L, unsigned long long *q, uint64_t nch) {
 #else
         const uint32_t k = (home + d) % kQSub;
 #endif
-#if MCK_QMASK
-        if (d > 0 && !have_mask) {
-            mask = __hip_atomic_load(q + kQMask * kQStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            have_mask = true;
-        }
-        if (!((mask >> k) & 1ull)) {
-#endif
         // sub-queue k owns chunks k, k + 8, k + 16, ...: every XCD streams
         // from the same moving window of the batch (contiguous per-XCD ranges
         // -- 8 windows far apart -- measured 8% slower on the headline batch)
         const uint64_t t = atomicAdd(q + k * kQStride, 1ull);
         if (k + t * kQSub < nch) return k + t * kQSub;
-#if MCK_QMASK
-        if (!have_mask || !((mask >> k) & 1ull)) atomicOr(q + kQMask * kQStride, 1ull << k);
-        }
-#endif
         atomicMax(&L->drained, d + 1);
         const uint32_t seen = lds_ld(&L->drained);
         d = seen > d + 1 ? seen : d + 1;

@@ -38,13 +38,19 @@ namespace {
 //   CRC(object) = Z^N(init) ^ XOR_c Z^(after_c)(L(chunk_c)) ^ xorout
 // where chunks of at most kChunk bytes tile every segment, L is the CRC with
 // zero init and no finalisation, N is the object's byte count and after_c the
-// number of object bytes that follow chunk c.  Two launches after zeroing the
-// output: one workgroup scans the segment lengths into byte and chunk prefix
-// sums (caller's workspace); then persistent waves stride over chunks, compute
-// L on 64 lanes with the payload kernels' step loop, shift it by after_c (at
-// most 12 table-operator applications, base-16 digits) and XOR it into
-// out[j] with an atomic -- XOR commutes, so the value is deterministic.  The
-// same launch adds each object's Z^N(init) ^ xorout term.
+// number of object bytes that follow chunk c.  Short scan launches write the
+// segment lengths' byte and chunk prefix sums (caller's workspace) and preset
+// out[j] = init ^ xorout (the CRC of an empty object); then persistent waves
+// take chunks, compute L on 64 lanes with the payload kernels' step loop,
+// shift it by after_c (at most 12 table-operator applications, base-16
+// digits) and XOR it into out[j] with an atomic -- XOR commutes, so the value
+// is deterministic.  The chunk that starts its object (object offset 0) runs
+// its step loop from the register `init` instead of 0 (R(init, M) =
+// R(0, M ^ init): init rides in its first W/8 bytes, or Z^n(init) is added
+// for a chunk shorter than that) and XORs init once more, cancelling the
+// preset's: Z^after(Z^n(init)) = Z^N(init), so the object term costs nothing
+// (round 3 added it in a launch of its own: ~6 us per call, plus a kernel
+// boundary).
 //
 // 256 KiB chunks: enough of them to fill the chip from a single GiB-sized
 // segment, while the shift (a few us of dependent scalar loads) stays a few
@@ -74,10 +80,11 @@ struct SegArgs {
 // Exclusive prefix sums of segment bytes (P) and chunk counts (C) in short
 // launches over blocks of kScanBlk segments (one workgroup streams only
 // ~20 GB/s, so a single-workgroup scan of 32768 segments took 48 us):
-// reduce (block totals; also zeroes the output the chunk passes XOR into),
-// top (exclusive scan of the block totals, one workgroup) and down (block-local
-// scan + block offset); up to 1 Mi segments, down does top's work itself
-// (two launches).  The totals also count segments whose chunks cannot
+// reduce (block totals; also presets the output the chunk passes XOR into,
+// and notes the object holding each block's first segment), top (exclusive
+// scan of the block totals, one workgroup) and down (block-local scan + block
+// offset, each segment's object); up to 1 Mi segments, down does top's work
+// itself (two launches).  The totals also count segments whose chunks cannot
 // all take the aligned loop (start not 16-B aligned or length not a multiple
 // of 1 KiB): the CRC-64 ragged pass returns at once when there are none.
 constexpr uint32_t kScanThreads = 256, kScanPer = 4, kScanBlk = kScanThreads * kScanPer;
@@ -118,11 +125,30 @@ __device__ __forceinline__ void block_scan2(uint64_t &p, uint64_t &c, uint64_t *
     *tc = sc;
 }
 
+constexpr uint64_t kNoObj = ~0ull;
+
+// preset: out[j] = init ^ xorout of the kernels' register form (W-bit words).
+// bobj (nullptr: not needed): the object holding each scan block's first
+// segment, kNoObj outside [first[0], first[nobj]) -- one writer per block: the
+// object whose segment range covers the block start.
 __global__ __launch_bounds__(kScanThreads) void seg_scan_reduce(const uint64_t *len, const uint64_t *addr, uint64_t nseg,
-                                                                uint64_t nb, uint64_t *tot, uint32_t *out,
-                                                                uint64_t out_words) {
-    for (uint64_t i = (uint64_t)blockIdx.x * kScanThreads + threadIdx.x; i < out_words; i += (uint64_t)gridDim.x * kScanThreads)
-        out[i] = 0;
+                                                                uint64_t nb, uint64_t *tot, void *out, uint64_t nobj,
+                                                                uint32_t width, uint64_t preset, const uint64_t *first,
+                                                                uint64_t *bobj) {
+    const uint64_t gtid = (uint64_t)blockIdx.x * kScanThreads + threadIdx.x, gstride = (uint64_t)gridDim.x * kScanThreads;
+    for (uint64_t j = gtid; j < nobj; j += gstride) {
+        if (width == 64) reinterpret_cast<uint64_t *>(out)[j] = preset;
+        else reinterpret_cast<uint32_t *>(out)[j] = (uint32_t)preset;
+        if (bobj) {
+            const uint64_t lo = first[j], hi = first[j + 1];
+            for (uint64_t b = (lo + kScanBlk - 1) / kScanBlk; b * kScanBlk < hi; b++) bobj[b] = j;
+        }
+    }
+    if (bobj) {
+        const uint64_t f0 = first[0], f1 = first[nobj];
+        for (uint64_t b = gtid; b < nb; b += gstride)
+            if (b * kScanBlk < f0 || b * kScanBlk >= f1) bobj[b] = kNoObj;
+    }
     uint64_t p = 0, c = 0, r = 0;
 #pragma unroll
     for (uint32_t e = 0; e < kScanPer; e++) {
@@ -182,20 +208,28 @@ __global__ __launch_bounds__(kScanThreads) void seg_scan_top(uint64_t *tot, uint
     }
 }
 
-constexpr uint64_t kNoObj = ~0ull;
-
 // Block offset pass.  FUSED (lists of at most kScanFusedBlocks blocks): the
 // top pass is folded in -- each block sums the raw totals of the blocks before
 // it (a few hundred words at most) and the last block writes the grand totals
 // and the ragged flag -- so the scan takes two launches instead of three.
 constexpr uint64_t kScanFusedBlocks = 1024;
 
+// Each segment's object (obj, the queue pass's map) without a search: the
+// objects touching the block are [bobj[b], bobj[b + 1]] (the objects of this
+// block's and the next block's first segments, from the reduce pass); a thread
+// per object writes the object's index over its segments in an LDS row of the
+// block (empty objects write nothing, so a segment gets the last object whose
+// range starts at or before it), and every thread then reads its own
+// segments' entries.  Round 3 ran a binary search over all of first[] in
+// global memory per segment: ~14 dependent loads, 15 of the pass's 17 us at
+// 32768 segments.
+
 template <bool FUSED>
 __global__ __launch_bounds__(kScanThreads) void seg_scan_down(const uint64_t *len, uint64_t nseg, const uint64_t *tot,
                                                               uint64_t nb, uint64_t *P, uint64_t *C,
                                                               unsigned long long *ragged, const uint64_t *first,
-                                                              uint64_t nobj, uint64_t *obj, uint32_t *map,
-                                                              uint64_t map_cap) {
+                                                              uint64_t nobj, uint64_t *obj, const uint64_t *bobj,
+                                                              uint32_t *map, uint64_t map_cap) {
     uint64_t off_p = 0, off_c = 0;
     uint32_t rag_all = 0;
     if constexpr (FUSED) {
@@ -238,16 +272,35 @@ __global__ __launch_bounds__(kScanThreads) void seg_scan_down(const uint64_t *le
     }
     uint64_t ep = off_p + p - p0, ec = off_c + c - c0;
     const uint64_t f0 = first[0], f1 = first[nobj];
+    // the object holding segment i: the last j with first[j] <= i (empty
+    // objects before it share its first index); only the queue pass reads it
+    // (obj == nullptr otherwise)
+    __shared__ uint64_t row[kScanBlk];
+    if (obj) {
+        const uint64_t s0 = (uint64_t)blockIdx.x * kScanBlk;
+        const uint64_t s1 = s0 + kScanBlk < nseg ? s0 + kScanBlk : nseg;
+        for (uint32_t t = threadIdx.x; t < kScanBlk; t += kScanThreads) row[t] = kNoObj;
+        __syncthreads();
+        const uint64_t lo_s = s0 > f0 ? s0 : f0, hi_s = s1 < f1 ? s1 : f1;
+        if (lo_s < hi_s) {
+            const uint64_t jb = s0 >= f0 ? bobj[blockIdx.x] : 0;
+            const uint64_t jn = blockIdx.x + 1 < nb ? bobj[blockIdx.x + 1] : kNoObj;
+            const uint64_t je = jn != kNoObj ? jn : nobj - 1;
+            for (uint64_t k = jb + threadIdx.x; k <= je; k += kScanThreads) {
+                const uint64_t a0 = first[k], a1 = first[k + 1];
+                const uint64_t lo = a0 > lo_s ? a0 : lo_s, hi = a1 < hi_s ? a1 : hi_s;
+                for (uint64_t i = lo; i < hi; i++) row[i - s0] = k;
+            }
+        }
+        __syncthreads();
+    }
 #pragma unroll
     for (uint32_t e = 0; e < kScanPer; e++) {
         const uint64_t i = (uint64_t)blockIdx.x * kScanBlk + threadIdx.x * kScanPer + e;
         if (i < nseg) {
             P[i] = ep;
             C[i] = ec;
-            // the object holding segment i: the last j with first[j] <= i
-            // (empty objects before it share its first index); only the
-            // queue pass reads it (nullptr otherwise)
-            if (obj) obj[i] = i >= f0 && i < f1 ? lower_bound_u64(first, nobj + 1, i + 1) - 1 : kNoObj;
+            if (obj) obj[i] = row[i - (uint64_t)blockIdx.x * kScanBlk];
             // chunk -> segment map, while it fits (the chunk passes check the
             // total against map_cap and search C otherwise)
             const uint64_t ce = ec + seg_chunks(l[e]);
@@ -283,8 +336,9 @@ struct ChunkWalk {
     }
 
     // Next chunk: its bytes [addr, addr + n) and, when its segment belongs to
-    // an object (*in), the object and the object bytes that follow it.
-    __device__ bool next(uint64_t *addr, uint64_t *n, bool *in, uint64_t *obj, uint64_t *after) {
+    // an object (*in), the object, the object bytes that follow it and
+    // whether it starts the object (*head).
+    __device__ bool next(uint64_t *addr, uint64_t *n, bool *in, uint64_t *obj, uint64_t *after, bool *head) {
         if (c >= c1) return false;
         while (a->C[s + 1] <= c) s++;  // skips empty segments
         const uint64_t off = (c - a->C[s]) * kChunk, L = a->len[s];
@@ -295,6 +349,7 @@ struct ChunkWalk {
             while (a->first[j + 1] <= s) j++;
             *obj = j;
             *after = a->P[a->first[j + 1]] - (a->P[s] + off + *n);
+            *head = a->P[s] + off == a->P[a->first[j]];
         }
         c++;
         return true;
@@ -316,11 +371,12 @@ struct ChunkWalk {
 #endif
 
 // Chunk c (< nchunks): its bytes [addr, addr + n) and, when its segment
-// belongs to an object (*in), the object and the object bytes after it.
-// c is wave-uniform, so every load is scalar.
+// belongs to an object (*in), the object, the object bytes after it and
+// whether it starts the object (*head).  c is wave-uniform, so every load is
+// scalar.
 __device__ __forceinline__ __attribute__((unused)) void seg_locate(const SegArgs &a, uint64_t c, uint64_t nchunks,
                                                                    uint64_t *addr, uint64_t *n, bool *in,
-                                                                   uint64_t *obj, uint64_t *after) {
+                                                                   uint64_t *obj, uint64_t *after, bool *head) {
     const uint64_t s = nchunks <= a.map_cap ? (uint64_t)a.map[c] : lower_bound_u64(a.C, a.nseg + 1, c + 1) - 1;
     const uint64_t off = (c - a.C[s]) * kChunk, L = a.len[s];
     *addr = a.addr[s] + off;
@@ -330,47 +386,32 @@ __device__ __forceinline__ __attribute__((unused)) void seg_locate(const SegArgs
     if (*in) {
         *obj = j;
         *after = a.P[a.first[j + 1]] - (a.P[s] + off + *n);
+        *head = a.P[s] + off == a.P[a.first[j]];
     }
 }
 
-// Each object's Z^N(init) ^ xorout term (N = its byte count), XORed into
-// out[j] next to the chunk terms.  Latency-bound (up to 12 dependent table
-// applications per object), no LDS: the CRC-64 ragged pass runs only this when
-// no chunk needs the ragged loop.
-template <int W>
-__device__ __forceinline__ void seg_object_terms(const SegArgs &a) {
-    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < a.nobj; j += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t N = a.P[a.first[j + 1]] - a.P[a.first[j]];
-        if constexpr (W == 32) {
-            const crc32_gpu_pack_t *pk = reinterpret_cast<const crc32_gpu_pack_t *>(a.pack);
-            const crc32_shift_pack_t *sp = reinterpret_cast<const crc32_shift_pack_t *>(a.shift);
-            atomicXor(reinterpret_cast<uint32_t *>(a.out) + j, shift32(sp, pk->init, N) ^ pk->xorout);
-        } else {
-            const crc64_gpu_pack_t *pk = reinterpret_cast<const crc64_gpu_pack_t *>(a.pack);
-            const crc64_shift_pack_t *sp = reinterpret_cast<const crc64_shift_pack_t *>(a.shift);
-            atomicXor(reinterpret_cast<unsigned long long *>(a.out) + j,
-                      (unsigned long long)(shift64(sp, pk->init, N) ^ pk->xorout));
-        }
-    }
-}
-
-// PART 0: every chunk + the object terms (CRC-32C: 140 KiB of LDS, one
-// workgroup per CU either way).  CRC-64 splits the chunks by shape: PART 1
-// takes the aligned ones with two workgroups per CU (8 waves/SIMD: the
-// VALU/LDS-bound loop needs them, and <= 64 VGPRs only fits the aligned
-// loop), PART 2 the ragged ones (if any) and the object terms.
+// PART 0: every chunk (CRC-32C: 140 KiB of LDS, one workgroup per CU either
+// way).  CRC-64, MCK_SEG_MERGED=1 (round 4): PART 3 takes every chunk from the
+// work queue in one 1024-thread workgroup per CU (128 VGPRs: the ragged loop
+// fits beside the aligned one; all operators in LDS).  MCK_SEG_MERGED=0 (round
+// 3) split the chunks by shape: PART 1 took the aligned ones with two
+// workgroups per CU (8 waves/SIMD, <= 64 VGPRs: only the aligned loop fits),
+// PART 2 the ragged ones in a launch of its own -- ~7 us per call even when
+// it found none (an early-exit launch of 256 x 1024 threads) -- while one
+// workgroup per CU ran the aligned CRC-64 loop as fast as two (C3, round 3:
+// +0.4% / +1.4%, profiles/r03/ab_crc64_one_wg_c3*.log).
 // (keyed W * 4 + PART: a comma inside __launch_bounds__ splits the macro)
 template <int KEY>
 constexpr int kSegWavesPerEU = KEY == 64 * 4 + 1 ? 8 : 1;
+#ifndef MCK_SEG_MERGED
+#define MCK_SEG_MERGED 1
+#endif
 
 constexpr uint64_t kSegNtBytes = 512ull << 20;
 
 template <int W, int PART>
 __global__ __launch_bounds__(1024, kSegWavesPerEU<W * 4 + PART>) void seg_kernel(SegArgs a) {
-    if (PART == 2 && *a.ragged == 0) {  // every chunk took the aligned pass: object terms only
-        seg_object_terms<W>(a);
-        return;
-    }
+    if (PART == 2 && *a.ragged == 0) return;  // every chunk takes the aligned pass
     constexpr int kWPB = 1024 / 64;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWPB + (threadIdx.x >> 6));
@@ -378,26 +419,26 @@ __global__ __launch_bounds__(1024, kSegWavesPerEU<W * 4 + PART>) void seg_kernel
     const uint64_t nchunks = uniform(a.C[a.nseg]);
     // the CRC-64 aligned chunk pass takes chunks from the work queue (the host
     // passes a slot; without one, for_each_unit strides statically)
-    constexpr bool kQueue = MCK_SEG_QUEUE && PART == 1;
+    constexpr bool kQueue = MCK_SEG_QUEUE && (PART == 1 || PART == 3);
     __shared__ WgQueue wgq;
     if (kQueue && threadIdx.x == 0) wg_queue_init(&wgq, a.queue, nchunks);
-    // Calls body(addr, n, j, after) for every chunk of this wave that belongs
-    // to an object; true in the first wave of a launch whose queue wait gave
-    // up (the caller's error word then gets +1: fail closed).
+    // Calls body(addr, n, j, after, head) for every chunk of this wave that
+    // belongs to an object; true in the first wave of a launch whose queue
+    // wait gave up (the caller's error word then gets +1: fail closed).
     auto chunks = [&](auto &&body) -> bool {
         if constexpr (kQueue) {
             return for_each_unit<true>(&wgq, a.queue, nchunks, wave, nw, [&](uint64_t c) {
                 uint64_t p, n, j = 0, after = 0;
-                bool in;
-                seg_locate(a, c, nchunks, &p, &n, &in, &j, &after);
-                if (in) body(p, n, j, after);
+                bool in, head = false;
+                seg_locate(a, c, nchunks, &p, &n, &in, &j, &after, &head);
+                if (in) body(p, n, j, after, head);
             });
         } else {
             ChunkWalk walk(a, wave, nw, nchunks);
-            uint64_t p, n, j, after;
-            bool in;
-            while (walk.next(&p, &n, &in, &j, &after))
-                if (in) body(p, n, j, after);
+            uint64_t p, n, j = 0, after = 0;
+            bool in, head = false;
+            while (walk.next(&p, &n, &in, &j, &after, &head))
+                if (in) body(p, n, j, after, head);
             return false;
         }
     };
@@ -411,19 +452,24 @@ __global__ __launch_bounds__(1024, kSegWavesPerEU<W * 4 + PART>) void seg_kernel
         const uint32_t lc0 = (lane & 31u) << 2, lc1 = lc0 | 0x10000u;
         uint32_t *out = reinterpret_cast<uint32_t *>(a.out);
         const bool nt = uniform(a.P[a.nseg]) >= kSegNtBytes;  // as for CRC-64 below
-        const bool faulted = chunks([&](uint64_t p, uint64_t n, uint64_t j, uint64_t after) {
+        const uint32_t init = pk->init;
+        const bool faulted = chunks([&](uint64_t p, uint64_t n, uint64_t j, uint64_t after, bool head) {
             const uint8_t *q = reinterpret_cast<const uint8_t *>(p);
             // whole rings of 1 KiB steps from a 16-B aligned start (the usual
             // bulk segment) take the aligned loop: no edge masks, no pad operator
             const bool aligned = p % 16 == 0 && n % (1024u * kRing) == 0 && n != 0;
-            uint32_t x = aligned && nt    ? payload32_aligned<6, true>(lds, q, n >> 10, lane, lc0, lc1, 0u)
-                         : aligned        ? payload32_aligned<6, false>(lds, q, n >> 10, lane, lc0, lc1, 0u)
-                                          : payload32_g64<false, Tab32<false>, true>(lds, pk, q, n, lane, lc0, lc1);
-            x = shift32(sp, uniform(x), after);
-            if (lane == 0) atomicXor(out + j, x);
+            // the object's first chunk starts from the register init (in its
+            // first 4 bytes; Z^n(init) for a shorter chunk)
+            const uint32_t reg = head && n >= 4 ? init : 0u;
+            uint32_t x = aligned && nt    ? payload32_aligned<6, true>(lds, q, n >> 10, lane, lc0, lc1, reg)
+                         : aligned        ? payload32_aligned<6, false>(lds, q, n >> 10, lane, lc0, lc1, reg)
+                                          : payload32_g64<false, Tab32<false>, true>(lds, pk, q, n, lane, lc0, lc1, reg);
+            x = uniform(x);
+            if (head && n < 4) x ^= pk->zinit[n];
+            x = shift32(sp, x, after);
+            if (lane == 0) atomicXor(out + j, head ? x ^ init : x);  // ^ init: cancels the preset's
         });
         if (faulted && lane == 0 && a.err_word) atomicAdd(a.err_word, 1u);
-        seg_object_terms<32>(a);
     } else {
         // aligned chunks under the 12-lookup fold: combine operators from
         // global memory (once per 256 KiB chunk), so two workgroups fit a CU
@@ -441,22 +487,26 @@ __global__ __launch_bounds__(1024, kSegWavesPerEU<W * 4 + PART>) void seg_kernel
         // branch per chunk: +3% on `seg` (duplicating the whole walk under one
         // branch measured the same and spills more).
         [[maybe_unused]] const bool nt = uniform(a.P[a.nseg]) >= kSegNtBytes;
-        const bool faulted = chunks([&](uint64_t p, uint64_t n, uint64_t j, uint64_t after) {
+        const uint64_t init = pk->init;
+        const bool faulted = chunks([&](uint64_t p, uint64_t n, uint64_t j, uint64_t after, bool head) {
             const uint8_t *q = reinterpret_cast<const uint8_t *>(p);
             const bool aligned = p % 16 == 0 && n % 1024 == 0;
-            if (aligned != (PART == 1)) return;
+            if (PART != 3 && aligned != (PART == 1)) return;
+            // the object's first chunk starts from the register init (in its
+            // first 8 bytes; Z^n(init) for a shorter, ragged chunk)
+            const uint64_t reg = head && n >= 8 ? init : 0ull;
             uint64_t x;
-            if constexpr (PART == 1)
-                x = nt ? payload64_aligned<6, true, OG>(lds, pk, q, (uint32_t)(n >> 10), lane, lc, 0ull)
-                       : payload64_aligned<6, false, OG>(lds, pk, q, (uint32_t)(n >> 10), lane, lc, 0ull);
+            if (PART == 1 || (PART == 3 && aligned))
+                x = nt ? payload64_aligned<6, true, OG>(lds, pk, q, (uint32_t)(n >> 10), lane, lc, reg)
+                       : payload64_aligned<6, false, OG>(lds, pk, q, (uint32_t)(n >> 10), lane, lc, reg);
             else
-                x = payload64_g64<false, true>(lds, pk, q, n, lane, lc);
-            x = shift64(sp, uniform(x), after);
-            if (lane == 0) atomicXor(out + j, (unsigned long long)x);
+                x = payload64_g64<false, true>(lds, pk, q, n, lane, lc, reg);
+            x = uniform(x);
+            if (!aligned && head && n < 8) x ^= pk->zinit[n];
+            x = shift64(sp, x, after);
+            if (lane == 0) atomicXor(out + j, (unsigned long long)(head ? x ^ init : x));  // ^ init: cancels the preset's
         });
         if (faulted && lane == 0 && a.err_word) atomicAdd(a.err_word, 1u);
-        if constexpr (PART == 1) return;
-        seg_object_terms<64>(a);
     }
 }
 
@@ -781,14 +831,15 @@ using namespace mck;
 extern "C" {
 
 // P, C (nseg + 1 each), the ragged flag (+ pad), 3 words per scan block, the
-// object of each segment (nseg), then the chunk -> segment map (u32 entries:
+// object of each scan block's first segment (1 word per block), the object of
+// each segment (nseg), then the chunk -> segment map (u32 entries:
 // 4 per segment + 64 Ki, i.e. lists averaging up to ~1 MiB per segment, or
 // one huge segment up to 16 GiB; none past 2^32 segments).  More than 2^40
 // segments (far beyond device memory) is rejected, so the size cannot wrap:
 // SIZE_MAX then makes any allocation of it fail.
 constexpr uint64_t kMaxSegs = 1ull << 40;
 uint64_t seg_map_cap(uint64_t nseg) { return nseg < (1ull << 32) ? 4 * nseg + 65536 : 0; }
-uint64_t seg_words(uint64_t nseg) { return 2 * (nseg + 1) + 2 + 3 * ((nseg + kScanBlk - 1) / kScanBlk) + nseg; }
+uint64_t seg_words(uint64_t nseg) { return 2 * (nseg + 1) + 2 + 4 * ((nseg + kScanBlk - 1) / kScanBlk) + nseg; }
 size_t mchecksum_gpu_segments_work_size(size_t nseg) {
     if ((uint64_t)nseg > kMaxSegs) return SIZE_MAX;
     return sizeof(uint64_t) * seg_words(nseg) + sizeof(uint32_t) * seg_map_cap(nseg);
@@ -826,7 +877,8 @@ int mchecksum_gpu_checksum_segments(const char *hash_method, const uint64_t *dev
     a.ragged = (const unsigned long long *)dev_work + 2 * (nseg + 1);
     const uint64_t nb = (nseg + kScanBlk - 1) / kScanBlk;
     uint64_t *tot = (uint64_t *)dev_work + 2 * (nseg + 1) + 2;
-    a.obj = tot + 3 * nb;
+    uint64_t *bobj = tot + 3 * nb;
+    a.obj = bobj + nb;
     a.map = reinterpret_cast<const uint32_t *>((const uint64_t *)dev_work + seg_words(nseg));
     // only the CRC-64 queue pass reads the map; MCHECKSUM_GPU_SEG_MAP_CAP caps
     // the part of it used (tests: 0 forces the search over C)
@@ -839,21 +891,26 @@ int mchecksum_gpu_checksum_segments(const char *hash_method, const uint64_t *dev
     a.pack = pack;
     a.shift = shift;
     a.err_word = error_word();
-    const uint64_t out_words = (uint64_t)nobj * (uint64_t)(width / 32);
-    // at least one block per scan block, and enough to zero the output quickly
-    uint64_t zgrid = (out_words + kScanThreads - 1) / kScanThreads;
+    // at least one block per scan block, and enough to preset the output quickly
+    uint64_t zgrid = ((uint64_t)nobj + kScanThreads - 1) / kScanThreads;
     zgrid = zgrid > 1024 ? 1024 : zgrid;
     const unsigned rgrid = (unsigned)(nb > zgrid ? nb : zgrid > 0 ? zgrid : 1);
-    hipError_t e = launch_kernel(seg_scan_reduce, dim3(rgrid), dim3(kScanThreads), s, nullptr, dev_seg_len, dev_seg_addr,
-                                 (uint64_t)nseg, nb, tot, (uint32_t *)dev_out, out_words);
+    // every object starts as the CRC of the empty message, init ^ xorout in
+    // the kernels' register form (MSB-first models: byte-reversed, swapped
+    // back with the outputs below)
+    const crc_rmodel_t rm = gpu_rmodel(mck_model_index(hash_method));
+    const uint64_t preset = rm.rinit ^ rm.xorout;
     uint64_t *obj_w = width == 64 && MCK_SEG_QUEUE ? (uint64_t *)a.obj : nullptr;
+    hipError_t e = launch_kernel(seg_scan_reduce, dim3(rgrid), dim3(kScanThreads), s, nullptr, dev_seg_len, dev_seg_addr,
+                                 (uint64_t)nseg, nb, tot, dev_out, (uint64_t)nobj, (uint32_t)width, preset, dev_obj_first,
+                                 obj_w ? bobj : nullptr);
     const char *scan3 = getenv("MCHECKSUM_GPU_SEG_SCAN3");  // tests: force the three-launch scan
     if (e != hipSuccess) {
     } else if (nb >= 1 && nb <= kScanFusedBlocks && !(scan3 && scan3[0] == '1')) {
         e = launch_kernel(seg_scan_down<true>, dim3((unsigned)nb), dim3(kScanThreads), s, nullptr, dev_seg_len,
                           (uint64_t)nseg, (const uint64_t *)tot, nb, (uint64_t *)a.P, (uint64_t *)a.C,
-                          (unsigned long long *)a.ragged, dev_obj_first, (uint64_t)nobj, obj_w, (uint32_t *)a.map,
-                          a.map_cap);
+                          (unsigned long long *)a.ragged, dev_obj_first, (uint64_t)nobj, obj_w, (const uint64_t *)bobj,
+                          (uint32_t *)a.map, a.map_cap);
     } else {
         e = launch_kernel(seg_scan_top, dim3(1), dim3(kScanThreads), s, nullptr, tot, nb,
                           (uint64_t)nseg, (uint64_t *)a.P, (uint64_t *)a.C, (unsigned long long *)a.ragged);
@@ -861,14 +918,28 @@ int mchecksum_gpu_checksum_segments(const char *hash_method, const uint64_t *dev
             e = launch_kernel(seg_scan_down<false>, dim3((unsigned)nb), dim3(kScanThreads), s, nullptr, dev_seg_len,
                               (uint64_t)nseg, (const uint64_t *)tot, nb, (uint64_t *)a.P, (uint64_t *)a.C,
                               (unsigned long long *)a.ragged, dev_obj_first, (uint64_t)nobj, obj_w,
-                              (uint32_t *)a.map, a.map_cap);
+                              (const uint64_t *)bobj, (uint32_t *)a.map, a.map_cap);
     }
     if (e != hipSuccess) return hip_err(e, "segment scan launch");
     if (width == 32) {
         e = launch_kernel(seg_kernel<32, 0>, dim3(c->cus), dim3(1024), s, nullptr, a);
+    } else if (MCK_SEG_MERGED) {
+        SlotRef sr = MCK_SEG_QUEUE ? queue_slot(c, stream) : SlotRef{};
+        a.queue = sr.q;
+        e = launch_kernel(seg_kernel<64, 3>, dim3(c->cus), dim3(1024), s, sr.done, a);
+        if (e != hipSuccess) {
+            slot_unissue(c, sr);
+            return hip_err(e, "segment kernel launch");
+        }
+        slot_issued(sr);
     } else {
-        // the aligned chunk pass takes the work queue; the ragged pass never
-        // touches the slot (a.queue is cleared for it)
+        // the ragged pass first (it returns at once when the scan found no
+        // ragged chunk; XOR commutes, so the order of the passes is free): the
+        // call then ends on the long aligned pass, one kernel boundary fewer
+        // after it.  Only the aligned pass takes the work queue.
+        a.queue = nullptr;
+        e = launch_kernel(seg_kernel<64, 2>, dim3(c->cus), dim3(1024), s, nullptr, a);
+        if (e != hipSuccess) return hip_err(e, "segment kernel launch");
         SlotRef sr = MCK_SEG_QUEUE ? queue_slot(c, stream) : SlotRef{};
         a.queue = sr.q;
         e = launch_kernel(seg_kernel<64, 1>, dim3(2 * c->cus), dim3(1024), s, sr.done, a);
@@ -877,8 +948,6 @@ int mchecksum_gpu_checksum_segments(const char *hash_method, const uint64_t *dev
             return hip_err(e, "segment kernel launch");
         }
         slot_issued(sr);
-        a.queue = nullptr;
-        e = launch_kernel(seg_kernel<64, 2>, dim3(c->cus), dim3(1024), s, nullptr, a);
     }
     if (e != hipSuccess) return hip_err(e, "segment kernel launch");
     // MSB-first model: the kernels' values are the CRCs byte-swapped (crc_gpu_layout.h)
