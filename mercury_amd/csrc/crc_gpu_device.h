@@ -135,9 +135,15 @@ enum OpsMode : int { kOpsLds = 0, kOpsGlobal = 1, kOpsMix = 2 };
 #ifndef MCK_RING64
 #define MCK_RING64 MCK_RING
 #endif
+// ... and with one workgroup per CU the combine operators fit in LDS beside
+// the tables (kL64Bytes), as in the merged segment pass (round 4).
+#ifndef MCK_CRC64_ONE_WG_OPS_LDS
+#define MCK_CRC64_ONE_WG_OPS_LDS 1
+#endif
 template <int W, int MODE, bool LIGHT = false>
 struct Shape {
-    static constexpr bool ops_global = W == 64 && MODE == 0 && (MCK_CRC64_SPLIT || MCK_CRC64_P6);  // 0 = kFixedAligned
+    static constexpr bool ops_global = W == 64 && MODE == 0 && (MCK_CRC64_SPLIT || MCK_CRC64_P6) &&
+                                       !(MCK_CRC64_ONE_WG && MCK_CRC64_ONE_WG_OPS_LDS);  // 0 = kFixedAligned
     static constexpr bool two = W == 64 && ((MODE == 0 && !MCK_CRC64_ONE_WG) || (MODE == 2 && kCrc64OffTwo));
     static constexpr int block = LIGHT ? kLightBlock : two ? MCK_BLOCK64 : kBlock;
     static constexpr int blocks_per_cu = LIGHT ? 8 : two ? 2 : 1;

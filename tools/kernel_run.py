@@ -41,6 +41,15 @@ elif a.config == "xdr":  # bench.py's xdr layout: hg_perf_proc_iovec messages in
         data[offs[:-1] + k] = ((lens >> (24 - 8 * k)) & 0xFF).to(torch.uint8)
     xout = torch.empty(count, dtype=torch.int32, device="cuda")
     run = lambda: G.checksum_xdr(method, data, offs, bench.XDR_IOVEC, out=xout)
+elif a.config == "seg":  # bench.py's segments layout: 4 scattered 256 KiB segments per 1 MiB object
+    from mercury_amd.workload import segment_slots
+    slen = length // 4
+    data = torch.empty(count * length + 64, dtype=torch.uint8, device="cuda")
+    G.fill_splitmix(data, seed)
+    slots = segment_slots(seed, count * 4)
+    batch = G.SegmentBatch([data[int(q) * slen:(int(q) + 1) * slen] for q in slots], np.arange(0, count * 4 + 1, 4))
+    sout = torch.empty(count, dtype=torch.int64, device="cuda")
+    run = lambda: batch.checksum(method, out=sout)
 elif length is None:
     from mercury_amd.workload import varlen_offsets
     off = varlen_offsets(seed, count)
