@@ -93,7 +93,8 @@ variants: $(COBJS) $(BUILD)/mchecksum_gpu_ext.o | $(BUILD)
 	@for v in $(VARIANTS); do n=$${v%%:*}; f=$$(echo $${v#*:} | tr , " "); \
 	  echo "variant $$n: $$f"; \
 	  $(HIPCC) $(HIPFLAGS) $$f $(INC) -c $(CSRC)/mchecksum_gpu.hip -o $(BUILD)/variants/gpu_$$n.o && \
-	  $(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $(BUILD)/variants/libmchecksum_$$n.so $(COBJS) $(BUILD)/variants/gpu_$$n.o $(BUILD)/mchecksum_gpu_ext.o -lpthread || exit 1; \
+	  $(HIPCC) $(HIPFLAGS) $$f $(INC) -c $(CSRC)/mchecksum_gpu_ext.hip -o $(BUILD)/variants/gpu_ext_$$n.o && \
+	  $(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $(BUILD)/variants/libmchecksum_$$n.so $(COBJS) $(BUILD)/variants/gpu_$$n.o $(BUILD)/variants/gpu_ext_$$n.o -lpthread || exit 1; \
 	done
 .PHONY: variants
 

@@ -126,11 +126,18 @@ constexpr int kRingOff64 = kCrc64OffTwo ? 4 : kRingOff;
 // or the butterflies (ops 1..6) in LDS and the rest global
 enum OpsMode : int { kOpsLds = 0, kOpsGlobal = 1, kOpsMix = 2 };
 
-// A/B knobs for the aligned CRC-64 loop (round 3): one 1024-thread workgroup
-// per CU instead of two (128 VGPRs instead of 64: no spills, room for a deeper
-// load ring, MCK_RING64) -- half the waves to hide the LDS latency.
+// The aligned CRC-64 loop runs one 1024-thread workgroup per CU (round 4;
+// round 3 ran two): 128 VGPRs instead of 64 (no spills, room for a deeper
+// load ring, MCK_RING64) and, with the LDS of a whole CU, the combine
+// operators in LDS beside the tables -- half the waves to hide the LDS
+// latency, which measured as well: C3 1.3786 -> 1.3421 ms (-2.6%), 1 and 1024
+// x 4 KiB calls 10.4 -> 9.2 / 9.6 us, one process, 8 rounds
+// (profiles/r04/ab_c3_onewg.log: "onewglds"; one WG with the operators still in
+// global memory, "onewg", gave -0.9% -- round 3's +0.4% / +1.4% A/Bs,
+// profiles/r03/ab_crc64_one_wg_c3*.log).  The merged segment pass runs the
+// same shape (mchecksum_gpu_ext.hip).  MCK_CRC64_ONE_WG=0 builds the two.
 #ifndef MCK_CRC64_ONE_WG
-#define MCK_CRC64_ONE_WG 0
+#define MCK_CRC64_ONE_WG 1
 #endif
 #ifndef MCK_RING64
 #define MCK_RING64 MCK_RING
@@ -288,13 +295,21 @@ __device__ __forceinline__ uint32_t chunk_log2(uint64_t n) {
 #ifndef MCK_QTAIL
 #define MCK_QTAIL 1
 #endif
+// A/B knobs (round 4): tail chunks 2^-MCK_QTAIL_SHIFT of a full one, over the
+// last MCK_QTAIL_CHUNKS full chunks per workgroup.
+#ifndef MCK_QTAIL_SHIFT
+#define MCK_QTAIL_SHIFT 2
+#endif
+#ifndef MCK_QTAIL_CHUNKS
+#define MCK_QTAIL_CHUNKS 1
+#endif
 struct ChunkPlan {
     uint32_t cl, sl;    // log2 of the full / tail chunk size
     uint64_t nbig, nch, big_end;
     __device__ __forceinline__ explicit ChunkPlan(uint64_t n) {
         cl = chunk_log2(n);
-        sl = MCK_QTAIL && cl >= 2 ? cl - 2 : cl;
-        const uint64_t tail = (uint64_t)gridDim.x << cl;
+        sl = MCK_QTAIL && cl >= MCK_QTAIL_SHIFT ? cl - MCK_QTAIL_SHIFT : cl;
+        const uint64_t tail = (uint64_t)MCK_QTAIL_CHUNKS * gridDim.x << cl;
         nbig = n > tail ? (n - tail) >> cl : 0;
         big_end = nbig << cl;
         nch = nbig + ((n - big_end + (1ull << sl) - 1) >> sl);
@@ -1593,11 +1608,16 @@ __device__ void fill_lds64(uint8_t *lds, const crc64_gpu_pack_t *pk) {
 __device__ __forceinline__ uint64_t lo64(uint4 v) { return (uint64_t)v.y << 32 | v.x; }
 __device__ __forceinline__ uint64_t hi64(uint4 v) { return (uint64_t)v.w << 32 | v.z; }
 
+// Load ring of the aligned CRC-64 loop: MCK_RING64_NT for the non-temporal
+// (>= 512 MiB) batches, MCK_RING64 otherwise (A/B knobs, round 4).
+#ifndef MCK_RING64_NT
+#define MCK_RING64_NT MCK_RING64
+#endif
 template <int LOG2G, bool NT, bool OG>
 __device__ __forceinline__ uint64_t payload64_aligned(const uint8_t *lds, const crc64_gpu_pack_t *pk, const uint8_t *p,
                                                       uint32_t K, uint32_t gl, uint32_t lc, uint64_t init) {
     constexpr int G = 1 << LOG2G;
-    constexpr int R = MCK_RING64;
+    constexpr int R = NT ? MCK_RING64_NT : MCK_RING64;
     Lane64 ln = lane64(lc);
     // global (address-space 1) loads: a flat load would also hold up every LDS wait
     const gbyte_t src = global_ptr(p, LOG2G == 6) + 16u * gl;

@@ -126,3 +126,65 @@ def test_threads_sharing_one_stream_alternate_the_slot_banks(gpu):
     r = subprocess.run([sys.executable, "-c", SHARED, ROOT], capture_output=True, text=True, timeout=110,
                        env=dict(os.environ, MCHECKSUM_GPU_LIGHT="0"))
     assert r.returncode == 0 and "shared stream ok" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
+
+
+PERTHREAD = r"""
+import sys, threading, ctypes, os
+import numpy as np
+import torch
+sys.path.insert(0, sys.argv[1])
+from mercury_amd import gpu as G
+from oracle import oracle as O
+hip = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so"))
+hip.hipStreamSynchronize.argtypes = [ctypes.c_void_p]
+PER_THREAD = 2  # hipStreamPerThread
+host = O.splitmix_bytes(8 << 20, 777)
+dev = torch.cat([torch.from_numpy(host).cuda(), torch.zeros(64, dtype=torch.uint8, device="cuda")])
+rng = np.random.default_rng(3)
+offs = np.zeros(3001, dtype=np.uint64)
+offs[1:] = np.cumsum(rng.integers(0, 2048, 3000))
+offs_d = torch.from_numpy(offs.astype(np.int64)).cuda()
+want = torch.from_numpy(O.batch_offsets("crc32c", host, offs, nthreads=4).astype(np.uint32).view(np.int32)).cuda()
+ITERS, NT = 40, 4
+outs = torch.zeros((NT, ITERS, 3000), dtype=torch.int32, device="cuda")
+torch.cuda.synchronize()
+st0 = G.queue_stats()
+barrier = threading.Barrier(NT)
+errors = []
+
+def worker(k):
+    try:
+        torch.cuda.set_device(0)
+        barrier.wait()
+        for it in range(ITERS):
+            G.checksum_offsets("crc32c", dev, offs_d, out=outs[k, it], stream=PER_THREAD)
+        assert hip.hipStreamSynchronize(PER_THREAD) == 0  # this thread's own per-thread stream
+    except Exception as e:  # reported below
+        errors.append((k, repr(e)))
+
+th = [threading.Thread(target=worker, args=(k,)) for k in range(NT)]
+for t in th:
+    t.start()
+for t in th:
+    t.join(timeout=90)
+assert not any(t.is_alive() for t in th), "a worker thread did not finish"
+torch.cuda.synchronize()
+assert not errors, errors[:5]
+st1 = G.queue_stats()
+bad = torch.nonzero((outs != want).any(dim=2)).tolist()
+assert not bad, bad[:8]
+assert st1["slot"] - st0["slot"] == NT * ITERS and st1["noslot"] == st0["noslot"], (st0, st1)
+assert G.queue_faults() == 0
+print("per-thread ok", st0, st1)
+"""
+
+
+def test_per_thread_default_stream_takes_the_queue(gpu):
+    """hipStreamPerThread is one handle naming a different stream in every host
+    thread.  Round 3 gave its launches no slot (a slot per handle could have
+    served two threads' launches at once); with slots held per launch (round
+    4) they take the work queue like any other eager launch: 4 threads x 40
+    queue batches on it, every one with a slot, every result exact."""
+    r = subprocess.run([sys.executable, "-c", PERTHREAD, ROOT], capture_output=True, text=True, timeout=110,
+                       env=dict(os.environ, MCHECKSUM_GPU_LIGHT="0"))
+    assert r.returncode == 0 and "per-thread ok" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
