@@ -287,7 +287,7 @@ __device__ __forceinline__ uint32_t chunk_log2(uint64_t n) {
 }
 
 // Chunk plan: ids [0, nbig) are full chunks of 2^cl units; the last
-// (about one full chunk per workgroup of) units go out as quarter chunks, ids
+// (about one full chunk per workgroup of) units go out as eighth chunks, ids
 // [nbig, nch), so a workgroup that fetches late holds little unstarted work
 // when the queue runs dry (MCK_QTAIL=0: full chunks throughout).  The highest
 // ids are handed out last (every sub-queue counts up), so the small chunks
@@ -295,10 +295,14 @@ __device__ __forceinline__ uint32_t chunk_log2(uint64_t n) {
 #ifndef MCK_QTAIL
 #define MCK_QTAIL 1
 #endif
-// A/B knobs (round 4): tail chunks 2^-MCK_QTAIL_SHIFT of a full one, over the
-// last MCK_QTAIL_CHUNKS full chunks per workgroup.
+// Tail chunks are 2^-MCK_QTAIL_SHIFT of a full one, over the last
+// MCK_QTAIL_CHUNKS full chunks per workgroup.  Eighths since round 4
+// (quarters before): never slower in two one-process A/Bs, headline -0.4% /
+// -0.6%, C3 -0.7%, seg -0.7%, C4 +-0 (profiles/r04/ab_qtail.log,
+// ab_round4_knobs.log: "t3"); sixteenths or single units lost 2% on C4 (one
+// fetch per unit), two full chunks per workgroup of tail was +-0.
 #ifndef MCK_QTAIL_SHIFT
-#define MCK_QTAIL_SHIFT 2
+#define MCK_QTAIL_SHIFT 3
 #endif
 #ifndef MCK_QTAIL_CHUNKS
 #define MCK_QTAIL_CHUNKS 1

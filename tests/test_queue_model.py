@@ -14,7 +14,7 @@ steps the device code takes.  A launch without a slot (graph captures, the
 per-thread stream, streams past the table: crc_gpu_device.h "Exclusivity")
 takes the static split and never touches any slot; the fail-closed fault flag
 is modelled too.  Fetch triggers, chunk sizes (chunk_log2, the
-quarter-size tail chunks of ChunkPlan), the
+eighth-size tail chunks of ChunkPlan), the
 round-robin sub-queues, the LDS ring recycling and the bank zeroing mirror the
 device code one to one.
 """
@@ -110,8 +110,8 @@ def _launch(spec, bank, rnd, res):
     cl = chunk_log2(n, grid)
     cu, lead = 1 << cl, max(1, (1 << cl) // 4) if (1 << cl) > 4 else 1
     # ChunkPlan: full chunks, then about one full chunk per workgroup of units
-    # in quarter chunks
-    sl = cl - 2 if cl >= 2 else cl
+    # in eighth chunks (MCK_QTAIL_SHIFT = 3)
+    sl = cl - 3 if cl >= 3 else cl
     tail = grid << cl
     nbig = (n - tail) >> cl if n > tail else 0
     big_end = nbig << cl
