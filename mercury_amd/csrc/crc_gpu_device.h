@@ -299,8 +299,8 @@ __device__ __forceinline__ uint32_t chunk_log2(uint64_t n) {
 // MCK_QTAIL_CHUNKS full chunks per workgroup.  Eighths since round 4
 // (quarters before): never slower in two one-process A/Bs, headline -0.4% /
 // -0.6%, C3 -0.7%, seg -0.7%, C4 +-0 (profiles/r04/ab_qtail.log,
-// ab_round4_knobs.log: "t3"); sixteenths or single units lost 2% on C4 (one
-// fetch per unit), two full chunks per workgroup of tail was +-0.
+// ab_round4_knobs.log: "t3"); single-unit tail chunks lost 2.3% on C4 (one
+// fetch per unit), two full chunks per workgroup of tail +0.5% on the headline.
 #ifndef MCK_QTAIL_SHIFT
 #define MCK_QTAIL_SHIFT 3
 #endif
