@@ -18,10 +18,13 @@
 //    host-order field values: a per-field schema says how to undo the XDR.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <random>
 #include <type_traits>
 
 #include "crc_gpu_device.h"
@@ -64,8 +67,10 @@ struct SegArgs {
     uint64_t nobj;
     const uint64_t *P, *C;  // workspace: byte / chunk exclusive prefix sums, nseg + 1 each
     const unsigned long long *ragged;  // workspace: non-zero if any chunk needs the ragged loop
-    // workspace: object of each segment (kNoObj outside [first[0], first[nobj]))
-    // and the segment of each chunk while the chunks fit map_cap
+    // workspace: per segment s, {its object j (kNoObj outside [first[0],
+    // first[nobj])), first[j], first[j + 1]} (3 words: the queue pass finds a
+    // chunk's object bounds in one round of loads), and the segment of each
+    // chunk while the chunks fit map_cap
     const uint64_t *obj;
     const uint32_t *map;
     uint64_t map_cap;
@@ -77,17 +82,26 @@ struct SegArgs {
     uint32_t *err_word;
 };
 
-// Exclusive prefix sums of segment bytes (P) and chunk counts (C) in short
-// launches over blocks of kScanBlk segments (one workgroup streams only
-// ~20 GB/s, so a single-workgroup scan of 32768 segments took 48 us):
-// reduce (block totals; also presets the output the chunk passes XOR into,
-// and notes the object holding each block's first segment), top (exclusive
-// scan of the block totals, one workgroup) and down (block-local scan + block
-// offset, each segment's object); up to 1 Mi segments, down does top's work
-// itself (two launches).  The totals also count segments whose chunks cannot
-// all take the aligned loop (start not 16-B aligned or length not a multiple
-// of 1 KiB): the CRC-64 ragged pass returns at once when there are none.
+// Exclusive prefix sums of segment bytes (P) and chunk counts (C), each
+// segment's object, the chunk -> segment map and the ragged flag, in ONE
+// launch over scan blocks of kScanBlk segments (round 4; one workgroup
+// streams only ~20 GB/s, so a single-workgroup scan of 32768 segments took
+// 48 us).  A block scans its own segments, publishes its aggregate, and finds
+// its offset by a decoupled look-back over the blocks before it: one wave
+// reads 64 predecessors' descriptors at once and sums aggregates back to the
+// nearest published inclusive prefix, then publishes its own inclusive prefix.
+// Descriptors carry the call's epoch (a process-wide counter from a random
+// seed), so a workspace left by an earlier call needs no clearing.  The wait
+// depends only on blocks dispatched before this one (a kernel's workgroups
+// are dispatched in order and run to completion), and is bounded: a give-up
+// is counted as a queue fault and reported on the caller's error word.
+// The totals also flag segments whose chunks cannot all take the aligned loop
+// (start not 16-B aligned or length not a multiple of 1 KiB).  The same
+// launch presets out[j] = init ^ xorout.  Round 3 ran this as a block-reduce
+// launch and a block-offset launch (4.8 + 8.5 us at 32768 segments, beside a
+// kernel boundary), round 2 as three.
 constexpr uint32_t kScanThreads = 256, kScanPer = 4, kScanBlk = kScanThreads * kScanPer;
+constexpr uint32_t kDescWords = 8;  // per scan block: flag, aggregate (p, c, r), inclusive (p, c, r), pad
 
 __device__ __forceinline__ uint64_t seg_chunks(uint64_t l) { return (l + kChunk - 1) / kChunk; }
 
@@ -127,180 +141,202 @@ __device__ __forceinline__ void block_scan2(uint64_t &p, uint64_t &c, uint64_t *
 
 constexpr uint64_t kNoObj = ~0ull;
 
-// preset: out[j] = init ^ xorout of the kernels' register form (W-bit words).
-// bobj (nullptr: not needed): the object holding each scan block's first
-// segment, kNoObj outside [first[0], first[nobj]) -- one writer per block: the
-// object whose segment range covers the block start.
-__global__ __launch_bounds__(kScanThreads) void seg_scan_reduce(const uint64_t *len, const uint64_t *addr, uint64_t nseg,
-                                                                uint64_t nb, uint64_t *tot, void *out, uint64_t nobj,
-                                                                uint32_t width, uint64_t preset, const uint64_t *first,
-                                                                uint64_t *bobj) {
-    const uint64_t gtid = (uint64_t)blockIdx.x * kScanThreads + threadIdx.x, gstride = (uint64_t)gridDim.x * kScanThreads;
-    for (uint64_t j = gtid; j < nobj; j += gstride) {
+// One wave: the largest index j < n with a[j] <= key (a sorted ascending,
+// a[0] <= key), by 64-ary narrowing: each round probes 64 evenly spaced
+// entries at once (3 rounds of loads for n = 8193 instead of 13 dependent ones).
+__device__ __forceinline__ uint64_t wave_last_le(const uint64_t *a, uint64_t n, uint64_t key, uint32_t lane) {
+    uint64_t lo = 0, hi = n;
+    while (hi - lo > 1) {
+        const uint64_t step = (hi - lo + 63) / 64;
+        const uint64_t idx = lo + (uint64_t)lane * step;
+        const unsigned long long m = __ballot(idx < hi && a[idx] <= key);
+        const uint64_t L = 63u - (uint32_t)__builtin_clzll(m);  // lane 0 (a[lo] <= key) is always set
+        lo += L * step;
+        hi = lo + step < hi ? lo + step : hi;
+    }
+    return lo;
+}
+
+__device__ __forceinline__ uint64_t ld_relaxed(const uint64_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_relaxed(uint64_t *p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+
+// Wave 0 of block b: publish (tp, tc, tr), look back, publish the inclusive
+// prefix; returns the exclusive prefix (bytes, chunks, ragged) in every lane.
+// false: the bounded wait gave up (fault counted).
+__device__ __forceinline__ bool seg_lookback(uint64_t *desc, uint64_t b, uint64_t epoch, uint64_t tp, uint64_t tc,
+                                             uint64_t tr, uint32_t lane, uint64_t *ep, uint64_t *ec, uint64_t *er) {
+    uint64_t *me = desc + kDescWords * b;
+    if (lane == 0) {
+        st_relaxed(me + 1, tp);
+        st_relaxed(me + 2, tc);
+        st_relaxed(me + 3, tr);
+        if (b == 0) {
+            st_relaxed(me + 4, tp);
+            st_relaxed(me + 5, tc);
+            st_relaxed(me + 6, tr);
+        }
+        __hip_atomic_store(me, epoch * 4 + (b == 0 ? 2u : 1u), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    uint64_t sp = 0, sc = 0, sr = 0;
+    bool ok = true;
+    if (b > 0) {
+        int64_t k = (int64_t)b - 1;  // window: blocks k, k - 1, ..., k - 63 (lane order)
+        uint32_t spins = 0;
+        for (;;) {
+            const int64_t idx = k - (int64_t)lane;
+            const uint64_t f = idx >= 0 ? ld_relaxed(desc + kDescWords * (uint64_t)idx) : epoch * 4 + 2;
+            const uint32_t state = (f >> 2) == epoch ? (uint32_t)(f & 3u) : 0u;
+            const unsigned long long incl = __ballot(state == 2), none = __ballot(state == 0);
+            const uint32_t S = incl ? (uint32_t)__builtin_ctzll(incl) : 64u;  // nearest inclusive prefix
+            const unsigned long long below = S >= 64 ? ~0ull : ((1ull << S) - 1);
+            if (none & below) {  // a nearer block has not published yet
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > (1u << 22)) {
+                    if (lane == 0) queue_fault(10, b, (uint64_t)k);
+                    ok = false;
+                    break;
+                }
+                continue;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            uint64_t vp = 0, vc = 0, vr = 0;
+            if (idx >= 0 && lane <= S) {
+                const uint64_t *d = desc + kDescWords * (uint64_t)idx + (lane == S ? 4 : 1);
+                vp = ld_relaxed(d);
+                vc = ld_relaxed(d + 1);
+                vr = ld_relaxed(d + 2);
+            }
+            sp += wave_sum(vp);
+            sc += wave_sum(vc);
+            sr |= wave_sum(vr);
+            if (S < 64) break;
+            k -= 64;
+        }
+        if (lane == 0) {
+            st_relaxed(me + 4, sp + tp);
+            st_relaxed(me + 5, sc + tc);
+            st_relaxed(me + 6, sr | tr);
+            __hip_atomic_store(me, epoch * 4 + 2, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    *ep = sp;
+    *ec = sc;
+    *er = sr ? 1u : 0u;
+    return ok;
+}
+
+// Each segment's object (obj, the queue pass's map) without a per-segment
+// search: waves 1 and 2 find the objects of the block's first and last
+// segments (wave_last_le over first[]); a thread per object in between writes
+// the object's index and bounds over its segments in LDS rows of the block
+// (empty objects write nothing, so a segment gets the last object whose range
+// starts at or before it), and every thread then reads its own segments'
+// entries.  Round 3 ran a binary search over all of first[] in global memory
+// per segment: ~14 dependent loads, 15 of the pass's 17 us at 32768 segments.
+__global__ __launch_bounds__(kScanThreads) void seg_scan(const uint64_t *len, const uint64_t *addr, uint64_t nseg,
+                                                         uint64_t *desc, uint64_t epoch, uint64_t *P, uint64_t *C,
+                                                         unsigned long long *ragged, const uint64_t *first,
+                                                         uint64_t nobj, uint64_t *obj, uint32_t *map, uint64_t map_cap,
+                                                         void *out, uint32_t width, uint64_t preset,
+                                                         uint32_t *err_word) {
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint64_t b = blockIdx.x, nb = gridDim.x;
+    const uint64_t s0 = b * kScanBlk, s1 = s0 + kScanBlk < nseg ? s0 + kScanBlk : nseg;
+    // every object starts as the CRC of the empty message (the chunk passes XOR into it)
+    for (uint64_t j = b * kScanThreads + threadIdx.x; j < nobj; j += nb * kScanThreads) {
         if (width == 64) reinterpret_cast<uint64_t *>(out)[j] = preset;
         else reinterpret_cast<uint32_t *>(out)[j] = (uint32_t)preset;
-        if (bobj) {
-            const uint64_t lo = first[j], hi = first[j + 1];
-            for (uint64_t b = (lo + kScanBlk - 1) / kScanBlk; b * kScanBlk < hi; b++) bobj[b] = j;
-        }
     }
-    if (bobj) {
-        const uint64_t f0 = first[0], f1 = first[nobj];
-        for (uint64_t b = gtid; b < nb; b += gstride)
-            if (b * kScanBlk < f0 || b * kScanBlk >= f1) bobj[b] = kNoObj;
-    }
-    uint64_t p = 0, c = 0, r = 0;
+    uint64_t l[kScanPer], p = 0, c = 0, r = 0;
 #pragma unroll
     for (uint32_t e = 0; e < kScanPer; e++) {
-        const uint64_t i = (uint64_t)blockIdx.x * kScanBlk + threadIdx.x * kScanPer + e;
-        if (i < nseg) {
-            const uint64_t l = len[i];
-            p += l;
-            c += seg_chunks(l);
-            r |= l && (l % 1024 != 0 || addr[i] % 16 != 0);
-        }
-    }
-    uint64_t tp, tc;
-    r = __any(r) ? 1 : 0;
-    block_scan2(p, c, &tp, &tc);
-    __shared__ uint32_t rag;
-    if (threadIdx.x == 0) rag = 0;
-    __syncthreads();
-    if (r && (threadIdx.x & 63u) == 0) atomicOr(&rag, 1u);
-    __syncthreads();
-    if (threadIdx.x == 0 && blockIdx.x < nb) {
-        tot[3 * blockIdx.x] = tp;
-        tot[3 * blockIdx.x + 1] = tc;
-        tot[3 * blockIdx.x + 2] = rag;
-    }
-}
-
-// One workgroup: block totals -> exclusive block offsets (in place); the
-// grand totals into P[nseg], C[nseg] and the ragged flag.
-__global__ __launch_bounds__(kScanThreads) void seg_scan_top(uint64_t *tot, uint64_t nb, uint64_t nseg, uint64_t *P,
-                                                             uint64_t *C, unsigned long long *ragged) {
-    uint64_t carry_p = 0, carry_c = 0, rag = 0;
-    for (uint64_t base = 0; base < nb; base += kScanThreads) {
-        const uint64_t b = base + threadIdx.x;
-        uint64_t p = b < nb ? tot[3 * b] : 0, c = b < nb ? tot[3 * b + 1] : 0;
-        rag |= b < nb ? tot[3 * b + 2] : 0;
-        const uint64_t p0 = p, c0 = c;
-        uint64_t tp, tc;
-        block_scan2(p, c, &tp, &tc);
-        if (b < nb) {
-            tot[3 * b] = carry_p + p - p0;
-            tot[3 * b + 1] = carry_c + c - c0;
-        }
-        carry_p += tp;
-        carry_c += tc;
-        __syncthreads();
-    }
-    rag = __any(rag) ? 1 : 0;
-    __shared__ uint32_t r;
-    if (threadIdx.x == 0) r = 0;
-    __syncthreads();
-    if (rag && (threadIdx.x & 63u) == 0) atomicOr(&r, 1u);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        P[nseg] = carry_p;
-        C[nseg] = carry_c;
-        *ragged = r;
-    }
-}
-
-// Block offset pass.  FUSED (lists of at most kScanFusedBlocks blocks): the
-// top pass is folded in -- each block sums the raw totals of the blocks before
-// it (a few hundred words at most) and the last block writes the grand totals
-// and the ragged flag -- so the scan takes two launches instead of three.
-constexpr uint64_t kScanFusedBlocks = 1024;
-
-// Each segment's object (obj, the queue pass's map) without a search: the
-// objects touching the block are [bobj[b], bobj[b + 1]] (the objects of this
-// block's and the next block's first segments, from the reduce pass); a thread
-// per object writes the object's index over its segments in an LDS row of the
-// block (empty objects write nothing, so a segment gets the last object whose
-// range starts at or before it), and every thread then reads its own
-// segments' entries.  Round 3 ran a binary search over all of first[] in
-// global memory per segment: ~14 dependent loads, 15 of the pass's 17 us at
-// 32768 segments.
-
-template <bool FUSED>
-__global__ __launch_bounds__(kScanThreads) void seg_scan_down(const uint64_t *len, uint64_t nseg, const uint64_t *tot,
-                                                              uint64_t nb, uint64_t *P, uint64_t *C,
-                                                              unsigned long long *ragged, const uint64_t *first,
-                                                              uint64_t nobj, uint64_t *obj, const uint64_t *bobj,
-                                                              uint32_t *map, uint64_t map_cap) {
-    uint64_t off_p = 0, off_c = 0;
-    uint32_t rag_all = 0;
-    if constexpr (FUSED) {
-        uint64_t sp = 0, sc = 0, sr = 0;
-        for (uint64_t k = threadIdx.x; k < nb; k += kScanThreads) {
-            if (k < blockIdx.x) {
-                sp += tot[3 * k];
-                sc += tot[3 * k + 1];
-            }
-            sr |= tot[3 * k + 2];
-        }
-        block_scan2(sp, sc, &off_p, &off_c);  // block sums of the preceding totals
-        __shared__ uint32_t r;
-        if (threadIdx.x == 0) r = 0;
-        __syncthreads();
-        if (__any(sr != 0) && (threadIdx.x & 63u) == 0) atomicOr(&r, 1u);
-        __syncthreads();
-        rag_all = r;
-    } else {
-        (void)nb;
-        (void)ragged;
-        off_p = tot[3 * blockIdx.x];
-        off_c = tot[3 * blockIdx.x + 1];
-    }
-    uint64_t l[kScanPer], p = 0, c = 0;
-#pragma unroll
-    for (uint32_t e = 0; e < kScanPer; e++) {
-        const uint64_t i = (uint64_t)blockIdx.x * kScanBlk + threadIdx.x * kScanPer + e;
+        const uint64_t i = s0 + threadIdx.x * kScanPer + e;
         l[e] = i < nseg ? len[i] : 0;
         p += l[e];
         c += seg_chunks(l[e]);
+        r |= i < nseg && l[e] && (l[e] % 1024 != 0 || addr[i] % 16 != 0);
+    }
+    // the objects touching this block (queue pass only)
+    const uint64_t f0 = first[0], f1 = first[nobj];
+    const uint64_t lo_s = s0 > f0 ? s0 : f0, hi_s = s1 < f1 ? s1 : f1;
+    __shared__ uint64_t jb_s, je_s;
+    if (obj && lo_s < hi_s) {
+        if (w == 1) {
+            const uint64_t jb = wave_last_le(first, nobj + 1, lo_s, lane);
+            if (lane == 0) jb_s = jb;
+        } else if (w == 2) {
+            const uint64_t je = wave_last_le(first, nobj + 1, hi_s - 1, lane);
+            if (lane == 0) je_s = je;
+        }
     }
     const uint64_t p0 = p, c0 = c;
     uint64_t tp, tc;
     block_scan2(p, c, &tp, &tc);
-    if (FUSED && blockIdx.x + 1 == nb && threadIdx.x == 0) {
-        P[nseg] = off_p + tp;
-        C[nseg] = off_c + tc;
-        *ragged = rag_all;
+    __shared__ uint32_t rag;
+    if (threadIdx.x == 0) rag = 0;
+    __syncthreads();
+    if (__any(r != 0) && lane == 0) atomicOr(&rag, 1u);
+    __syncthreads();
+    __shared__ uint64_t ex[3];
+    if (w == 0) {
+        uint64_t ep, ec, er;
+        const bool ok = seg_lookback(desc, b, epoch, tp, tc, rag, lane, &ep, &ec, &er);
+        if (lane == 0) {
+            ex[0] = ep;
+            ex[1] = ec;
+            ex[2] = er;
+            if (!ok && err_word) atomicAdd(err_word, 1u);  // fail closed: the scan is not trustworthy
+        }
     }
-    uint64_t ep = off_p + p - p0, ec = off_c + c - c0;
-    const uint64_t f0 = first[0], f1 = first[nobj];
-    // the object holding segment i: the last j with first[j] <= i (empty
-    // objects before it share its first index); only the queue pass reads it
-    // (obj == nullptr otherwise)
+    __syncthreads();
+    if (b + 1 == nb && threadIdx.x == 0) {
+        P[nseg] = ex[0] + tp;
+        C[nseg] = ex[1] + tc;
+        *ragged = ex[2] | rag;
+    }
+    uint64_t ep = ex[0] + p - p0, ec = ex[1] + c - c0;
     __shared__ uint64_t row[kScanBlk];
+    __shared__ uint64_t row_f0[kScanBlk], row_f1[kScanBlk];  // the object's first[j], first[j + 1]
     if (obj) {
-        const uint64_t s0 = (uint64_t)blockIdx.x * kScanBlk;
-        const uint64_t s1 = s0 + kScanBlk < nseg ? s0 + kScanBlk : nseg;
         for (uint32_t t = threadIdx.x; t < kScanBlk; t += kScanThreads) row[t] = kNoObj;
         __syncthreads();
-        const uint64_t lo_s = s0 > f0 ? s0 : f0, hi_s = s1 < f1 ? s1 : f1;
         if (lo_s < hi_s) {
-            const uint64_t jb = s0 >= f0 ? bobj[blockIdx.x] : 0;
-            const uint64_t jn = blockIdx.x + 1 < nb ? bobj[blockIdx.x + 1] : kNoObj;
-            const uint64_t je = jn != kNoObj ? jn : nobj - 1;
+            const uint64_t jb = jb_s, je = je_s;
             for (uint64_t k = jb + threadIdx.x; k <= je; k += kScanThreads) {
                 const uint64_t a0 = first[k], a1 = first[k + 1];
                 const uint64_t lo = a0 > lo_s ? a0 : lo_s, hi = a1 < hi_s ? a1 : hi_s;
-                for (uint64_t i = lo; i < hi; i++) row[i - s0] = k;
+                for (uint64_t i = lo; i < hi; i++) {
+                    row[i - s0] = k;
+                    row_f0[i - s0] = a0;
+                    row_f1[i - s0] = a1;
+                }
             }
         }
         __syncthreads();
     }
 #pragma unroll
     for (uint32_t e = 0; e < kScanPer; e++) {
-        const uint64_t i = (uint64_t)blockIdx.x * kScanBlk + threadIdx.x * kScanPer + e;
+        const uint64_t i = s0 + threadIdx.x * kScanPer + e;
         if (i < nseg) {
             P[i] = ep;
             C[i] = ec;
-            if (obj) obj[i] = row[i - (uint64_t)blockIdx.x * kScanBlk];
+            if (obj) {
+                const uint64_t t = i - s0;
+                obj[3 * i] = row[t];
+                if (row[t] != kNoObj) {
+                    obj[3 * i + 1] = row_f0[t];
+                    obj[3 * i + 2] = row_f1[t];
+                }
+            }
             // chunk -> segment map, while it fits (the chunk passes check the
             // total against map_cap and search C otherwise)
             const uint64_t ce = ec + seg_chunks(l[e]);
@@ -378,15 +414,24 @@ __device__ __forceinline__ __attribute__((unused)) void seg_locate(const SegArgs
                                                                    uint64_t *addr, uint64_t *n, bool *in,
                                                                    uint64_t *obj, uint64_t *after, bool *head) {
     const uint64_t s = nchunks <= a.map_cap ? (uint64_t)a.map[c] : lower_bound_u64(a.C, a.nseg + 1, c + 1) - 1;
-    const uint64_t off = (c - a.C[s]) * kChunk, L = a.len[s];
+    // (a scan whose look-back gave up -- reported on the error word -- leaves
+    // maps that may not fit: such a chunk is skipped, never read out of bounds)
+    const uint64_t cs = s < a.nseg ? a.C[s] : ~0ull, L = s < a.nseg ? a.len[s] : 0;
+    const uint64_t off = (c - cs) * kChunk;
+    if (cs > c || off >= L) {
+        *in = false;
+        return;
+    }
     *addr = a.addr[s] + off;
     *n = L - off < kChunk ? L - off : kChunk;
-    const uint64_t j = a.obj[s];
+    const uint64_t *o3 = a.obj + 3 * s;  // {j, first[j], first[j + 1]}
+    const uint64_t j = o3[0];
     *in = j != kNoObj;
     if (*in) {
         *obj = j;
-        *after = a.P[a.first[j + 1]] - (a.P[s] + off + *n);
-        *head = a.P[s] + off == a.P[a.first[j]];
+        const uint64_t at = a.P[s] + off;
+        *after = a.P[o3[2]] - (at + *n);
+        *head = at == a.P[o3[1]];
     }
 }
 
@@ -830,16 +875,29 @@ using namespace mck;
 
 extern "C" {
 
-// P, C (nseg + 1 each), the ragged flag (+ pad), 3 words per scan block, the
-// object of each scan block's first segment (1 word per block), the object of
-// each segment (nseg), then the chunk -> segment map (u32 entries:
+// P, C (nseg + 1 each), the ragged flag (+ pad), the look-back descriptor of
+// each scan block (kDescWords), each segment's object and its bounds in
+// first[] (3 nseg), then the chunk -> segment map (u32 entries:
 // 4 per segment + 64 Ki, i.e. lists averaging up to ~1 MiB per segment, or
 // one huge segment up to 16 GiB; none past 2^32 segments).  More than 2^40
 // segments (far beyond device memory) is rejected, so the size cannot wrap:
 // SIZE_MAX then makes any allocation of it fail.
 constexpr uint64_t kMaxSegs = 1ull << 40;
 uint64_t seg_map_cap(uint64_t nseg) { return nseg < (1ull << 32) ? 4 * nseg + 65536 : 0; }
-uint64_t seg_words(uint64_t nseg) { return 2 * (nseg + 1) + 2 + 4 * ((nseg + kScanBlk - 1) / kScanBlk) + nseg; }
+// scan blocks of a list (one at least: the scan launch writes the totals)
+uint64_t seg_blocks(uint64_t nseg) { return nseg ? (nseg + kScanBlk - 1) / kScanBlk : 1; }
+uint64_t seg_words(uint64_t nseg) { return 2 * (nseg + 1) + 2 + kDescWords * seg_blocks(nseg) + 3 * nseg; }
+// The scan's look-back epochs: a process-wide counter from a random seed, so a
+// workspace's descriptors from any earlier call (this process or, through
+// reused memory, another) never match the current call's.
+uint64_t scan_epoch() {
+    static std::atomic<uint64_t> ctr{[] {
+        std::random_device rd;
+        const uint64_t seed = ((uint64_t)rd() << 32 ^ rd() ^ (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count());
+        return (seed & ((1ull << 60) - 1)) | 1ull;
+    }()};
+    return ctr.fetch_add(1, std::memory_order_relaxed) & ((1ull << 61) - 1);
+}
 size_t mchecksum_gpu_segments_work_size(size_t nseg) {
     if ((uint64_t)nseg > kMaxSegs) return SIZE_MAX;
     return sizeof(uint64_t) * seg_words(nseg) + sizeof(uint32_t) * seg_map_cap(nseg);
@@ -875,10 +933,9 @@ int mchecksum_gpu_checksum_segments(const char *hash_method, const uint64_t *dev
     a.P = (const uint64_t *)dev_work;
     a.C = (const uint64_t *)dev_work + (nseg + 1);
     a.ragged = (const unsigned long long *)dev_work + 2 * (nseg + 1);
-    const uint64_t nb = (nseg + kScanBlk - 1) / kScanBlk;
-    uint64_t *tot = (uint64_t *)dev_work + 2 * (nseg + 1) + 2;
-    uint64_t *bobj = tot + 3 * nb;
-    a.obj = bobj + nb;
+    const uint64_t nb = seg_blocks(nseg);
+    uint64_t *desc = (uint64_t *)dev_work + 2 * (nseg + 1) + 2;
+    a.obj = desc + kDescWords * nb;
     a.map = reinterpret_cast<const uint32_t *>((const uint64_t *)dev_work + seg_words(nseg));
     // only the CRC-64 queue pass reads the map; MCHECKSUM_GPU_SEG_MAP_CAP caps
     // the part of it used (tests: 0 forces the search over C)
@@ -891,35 +948,16 @@ int mchecksum_gpu_checksum_segments(const char *hash_method, const uint64_t *dev
     a.pack = pack;
     a.shift = shift;
     a.err_word = error_word();
-    // at least one block per scan block, and enough to preset the output quickly
-    uint64_t zgrid = ((uint64_t)nobj + kScanThreads - 1) / kScanThreads;
-    zgrid = zgrid > 1024 ? 1024 : zgrid;
-    const unsigned rgrid = (unsigned)(nb > zgrid ? nb : zgrid > 0 ? zgrid : 1);
     // every object starts as the CRC of the empty message, init ^ xorout in
     // the kernels' register form (MSB-first models: byte-reversed, swapped
     // back with the outputs below)
     const crc_rmodel_t rm = gpu_rmodel(mck_model_index(hash_method));
     const uint64_t preset = rm.rinit ^ rm.xorout;
     uint64_t *obj_w = width == 64 && MCK_SEG_QUEUE ? (uint64_t *)a.obj : nullptr;
-    hipError_t e = launch_kernel(seg_scan_reduce, dim3(rgrid), dim3(kScanThreads), s, nullptr, dev_seg_len, dev_seg_addr,
-                                 (uint64_t)nseg, nb, tot, dev_out, (uint64_t)nobj, (uint32_t)width, preset, dev_obj_first,
-                                 obj_w ? bobj : nullptr);
-    const char *scan3 = getenv("MCHECKSUM_GPU_SEG_SCAN3");  // tests: force the three-launch scan
-    if (e != hipSuccess) {
-    } else if (nb >= 1 && nb <= kScanFusedBlocks && !(scan3 && scan3[0] == '1')) {
-        e = launch_kernel(seg_scan_down<true>, dim3((unsigned)nb), dim3(kScanThreads), s, nullptr, dev_seg_len,
-                          (uint64_t)nseg, (const uint64_t *)tot, nb, (uint64_t *)a.P, (uint64_t *)a.C,
-                          (unsigned long long *)a.ragged, dev_obj_first, (uint64_t)nobj, obj_w, (const uint64_t *)bobj,
-                          (uint32_t *)a.map, a.map_cap);
-    } else {
-        e = launch_kernel(seg_scan_top, dim3(1), dim3(kScanThreads), s, nullptr, tot, nb,
-                          (uint64_t)nseg, (uint64_t *)a.P, (uint64_t *)a.C, (unsigned long long *)a.ragged);
-        if (e == hipSuccess && nb)
-            e = launch_kernel(seg_scan_down<false>, dim3((unsigned)nb), dim3(kScanThreads), s, nullptr, dev_seg_len,
-                              (uint64_t)nseg, (const uint64_t *)tot, nb, (uint64_t *)a.P, (uint64_t *)a.C,
-                              (unsigned long long *)a.ragged, dev_obj_first, (uint64_t)nobj, obj_w,
-                              (const uint64_t *)bobj, (uint32_t *)a.map, a.map_cap);
-    }
+    hipError_t e = launch_kernel(seg_scan, dim3((unsigned)nb), dim3(kScanThreads), s, nullptr, dev_seg_len, dev_seg_addr,
+                                 (uint64_t)nseg, desc, scan_epoch(), (uint64_t *)a.P, (uint64_t *)a.C,
+                                 (unsigned long long *)a.ragged, dev_obj_first, (uint64_t)nobj, obj_w, (uint32_t *)a.map,
+                                 a.map_cap, dev_out, (uint32_t)width, preset, a.err_word);
     if (e != hipSuccess) return hip_err(e, "segment scan launch");
     if (width == 32) {
         e = launch_kernel(seg_kernel<32, 0>, dim3(c->cus), dim3(1024), s, nullptr, a);

@@ -263,7 +263,7 @@ class SegmentBatch:
                                                      np.asarray(lens, dtype=np.int64), first])).to(self.device)
         self.work = torch.empty((_lib().mchecksum_gpu_segments_work_size(self.nseg) + 7) // 8, dtype=torch.int64,
                                 device=self.device)
-        self._last = None  # (stream handle, stream) of the last call
+        self._last = None  # (stream handle, its torch stream, event after the call or None) of the last call
 
     def checksum(self, method: str, out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
         if out is None:
@@ -280,17 +280,26 @@ class SegmentBatch:
             s = (torch.cuda.ExternalStream(h) if h else torch.cuda.default_stream(self.device)) if track else None
             if track and self._last is not None and self._last[0] != h:
                 # the workspace is still the previous call's: this stream waits
-                # for everything queued so far on the previous call's stream
-                # (recorded now, at the switch, instead of an event after every
-                # call -- a marker packet between the kernels costs ~3 us)
-                ev = torch.cuda.Event()
-                ev.record(self._last[1])
+                # for it.  On a torch stream (never destroyed: torch's streams
+                # come from its pool) the event is recorded now, at the switch,
+                # after everything queued so far -- not after every call (a
+                # marker packet between the kernels costs ~3 us); a raw handle
+                # may be destroyed by then, so its event was recorded right
+                # after the call.
+                ev = self._last[2]
+                if ev is None:
+                    ev = torch.cuda.Event()
+                    ev.record(self._last[1])
                 s.wait_event(ev)
             rc = _lib().mchecksum_gpu_checksum_segments(method.encode(), base, base + 8 * n, n, base + 16 * n,
                                                         self.nobj, self.work.data_ptr(), self.work.numel() * 8,
                                                         out.data_ptr(), h)
             if rc == 0 and track:
-                self._last = (h, s)
+                ev = None
+                if stream is not None and not hasattr(stream, "cuda_stream"):  # a raw hipStream_t
+                    ev = torch.cuda.Event()
+                    ev.record(s)
+                self._last = (h, s, ev)
         if rc != 0:
             _err(rc, "mchecksum_gpu_checksum_segments")
         return out

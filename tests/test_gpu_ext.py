@@ -220,22 +220,33 @@ def test_core_headers_reject_wide_methods(gpu):
 
 
 @pytest.mark.parametrize("method", ["crc32c", "crc64"])
-@pytest.mark.parametrize("scan3", [False, True])
-def test_segments_long_lists_multi_block_scan(gpu, buf, oracle_mod, method, scan3, monkeypatch):
-    """300000 short segments (the prefix scan runs in 293 blocks: the fused
-    block-offset pass sums up to 292 preceding totals; scan3 forces the
-    three-launch scan, whose top pass takes two tiles) and an all-aligned list
-    (every chunk on the aligned pass: the CRC-64 ragged pass returns at once)."""
-    if scan3:
-        monkeypatch.setenv("MCHECKSUM_GPU_SEG_SCAN3", "1")
+@pytest.mark.parametrize("layout", ["per5", "one_object", "empties_subrange"])
+def test_segments_long_lists_multi_block_scan(gpu, buf, oracle_mod, method, layout):
+    """300000 short segments: the single-pass scan runs in 293 blocks, each
+    looking back over up to 292 predecessors (windows of 64).  Object tables:
+    5 segments each; ONE object over all 293 blocks (every block's objects are
+    found by the 64-ary search, the object's rows written across blocks); and
+    runs of empty objects with a table covering only part of the list
+    (segments outside it belong to no object)."""
     host = _host(buf)
     rng = np.random.default_rng(91)
     lens = rng.integers(0, 65, 300000)
     offs = rng.integers(0, buf.numel() - 128, 300000)
-    first = list(range(0, 300001, 5))
+    if layout == "per5":
+        first = list(range(0, 300001, 5))
+    elif layout == "one_object":
+        first = [0, 300000]
+    else:
+        cuts = np.sort(rng.integers(1000, 299000, 20000))
+        cuts = np.repeat(cuts, rng.integers(1, 4, cuts.size))  # repeated cuts: runs of empty objects
+        first = [1000] + [int(x) for x in cuts] + [299000]
     views = [buf[int(o):int(o) + int(n)] for o, n in zip(offs, lens)]
     got = gpu.as_unsigned(gpu.checksum_segments(method, views, first))
-    for j in list(range(0, 60000, 97)) + [59999]:
+    nobj = len(first) - 1
+    check = sorted(set(list(range(0, nobj, max(1, nobj // 600))) + [nobj - 1]))
+    if layout == "empties_subrange":
+        check += [j for j in range(nobj) if first[j] == first[j + 1]][:50]
+    for j in check:
         b = b"".join(host[int(offs[s]):int(offs[s]) + int(lens[s])].tobytes() for s in range(first[j], first[j + 1]))
         assert int(got[j]) == oracle_mod.crc(method, np.frombuffer(b, dtype=np.uint8)), j
     segs = [(16 * int(o), 4096) for o in rng.integers(0, (buf.numel() - 8192) // 16, 3000)]
@@ -258,6 +269,37 @@ def test_segments_large_batch_non_temporal(gpu, buf, oracle_mod, method):
     got = gpu.as_unsigned(gpu.checksum_segments(method, [buf[o:o + n] for o, n in segs], first)).tolist()
     for j in (0, 1, 17, 80, 159):
         assert got[j] == _want(oracle_mod, method, host, segs[first[j]:first[j + 1]], [0, 4])[0], j
+
+
+def test_segment_batch_raw_stream_destroyed_between_calls(gpu, buf, oracle_mod):
+    """A SegmentBatch called on a raw hipStream_t that the caller then destroys,
+    and next on another raw stream: the guard event of the first call was
+    recorded right after it (a raw handle may be gone by the next call), so
+    the second call waits on it safely and both results equal the oracle."""
+    import ctypes
+    import os
+    import torch
+    L = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so"))
+    L.hipStreamCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
+    L.hipStreamDestroy.argtypes = [ctypes.c_void_p]
+    host = _host(buf)
+    rng = np.random.default_rng(405)
+    segs, first = _objects(rng, buf.numel() - 64, 60)
+    batch = gpu.SegmentBatch([buf[o:o + n] for o, n in segs], first)
+    want = _want(oracle_mod, "crc64", host, segs, first)
+    outs = []
+    torch.cuda.synchronize()
+    for rep in range(6):
+        h = ctypes.c_void_p()
+        assert L.hipStreamCreateWithFlags(ctypes.byref(h), 1) == 0
+        o = torch.zeros(len(first) - 1, dtype=torch.int64, device="cuda")
+        torch.cuda.synchronize()  # o's zeroing done before the raw stream writes it
+        batch.checksum("crc64", out=o, stream=h.value)
+        assert L.hipStreamDestroy(h.value) == 0  # with the call possibly still in flight
+        outs.append(o)
+    torch.cuda.synchronize()
+    for o in outs:
+        assert gpu.as_unsigned(o).tolist() == want
 
 
 def test_segment_batch_calls_on_two_streams(gpu, buf, oracle_mod):
