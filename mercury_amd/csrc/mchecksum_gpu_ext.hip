@@ -173,7 +173,8 @@ __device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
 // prefix; returns the exclusive prefix (bytes, chunks, ragged) in every lane.
 // false: the bounded wait gave up (fault counted).
 __device__ __forceinline__ bool seg_lookback(uint64_t *desc, uint64_t b, uint64_t epoch, uint64_t tp, uint64_t tc,
-                                             uint64_t tr, uint32_t lane, uint64_t *ep, uint64_t *ec, uint64_t *er) {
+                                             uint64_t tr, uint32_t lane, uint64_t *ep, uint64_t *ec, uint64_t *er,
+                                             uint64_t fault_block) {
     uint64_t *me = desc + kDescWords * b;
     if (lane == 0) {
         st_relaxed(me + 1, tp);
@@ -192,6 +193,15 @@ __device__ __forceinline__ bool seg_lookback(uint64_t *desc, uint64_t b, uint64_
         int64_t k = (int64_t)b - 1;  // window: blocks k, k - 1, ..., k - 63 (lane order)
         uint32_t spins = 0;
         for (;;) {
+#if MCK_QFAULT_TEST
+            if (b == fault_block) {  // injected give-up (test builds, MCHECKSUM_GPU_QFAULT_SCAN)
+                if (lane == 0) queue_fault(11, b, 0);
+                ok = false;
+                break;
+            }
+#else
+            (void)fault_block;
+#endif
             const int64_t idx = k - (int64_t)lane;
             const uint64_t f = idx >= 0 ? ld_relaxed(desc + kDescWords * (uint64_t)idx) : epoch * 4 + 2;
             const uint32_t state = (f >> 2) == epoch ? (uint32_t)(f & 3u) : 0u;
@@ -247,7 +257,7 @@ __global__ __launch_bounds__(kScanThreads) void seg_scan(const uint64_t *len, co
                                                          unsigned long long *ragged, const uint64_t *first,
                                                          uint64_t nobj, uint64_t *obj, uint32_t *map, uint64_t map_cap,
                                                          void *out, uint32_t width, uint64_t preset,
-                                                         uint32_t *err_word) {
+                                                         uint32_t *err_word, uint64_t fault_block) {
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
     const uint64_t b = blockIdx.x, nb = gridDim.x;
     const uint64_t s0 = b * kScanBlk, s1 = s0 + kScanBlk < nseg ? s0 + kScanBlk : nseg;
@@ -289,7 +299,7 @@ __global__ __launch_bounds__(kScanThreads) void seg_scan(const uint64_t *len, co
     __shared__ uint64_t ex[3];
     if (w == 0) {
         uint64_t ep, ec, er;
-        const bool ok = seg_lookback(desc, b, epoch, tp, tc, rag, lane, &ep, &ec, &er);
+        const bool ok = seg_lookback(desc, b, epoch, tp, tc, rag, lane, &ep, &ec, &er, fault_block);
         if (lane == 0) {
             ex[0] = ep;
             ex[1] = ec;
@@ -376,13 +386,19 @@ struct ChunkWalk {
     // whether it starts the object (*head).
     __device__ bool next(uint64_t *addr, uint64_t *n, bool *in, uint64_t *obj, uint64_t *after, bool *head) {
         if (c >= c1) return false;
-        while (a->C[s + 1] <= c) s++;  // skips empty segments
-        const uint64_t off = (c - a->C[s]) * kChunk, L = a->len[s];
+        while (s < a->nseg && a->C[s + 1] <= c) s++;  // skips empty segments
+        const uint64_t cs = s < a->nseg ? a->C[s] : ~0ull, L = s < a->nseg ? a->len[s] : 0;
+        const uint64_t off = (c - cs) * kChunk;
+        if (cs > c || off >= L) {  // maps of a failed scan (reported): skip, never read out of bounds
+            *in = false;
+            c++;
+            return true;
+        }
         *addr = a->addr[s] + off;
         *n = L - off < kChunk ? L - off : kChunk;
         *in = s >= a->first[0] && s < a->first[a->nobj];
         if (*in) {
-            while (a->first[j + 1] <= s) j++;
+            while (j + 1 < a->nobj && a->first[j + 1] <= s) j++;
             *obj = j;
             *after = a->P[a->first[j + 1]] - (a->P[s] + off + *n);
             *head = a->P[s] + off == a->P[a->first[j]];
@@ -884,6 +900,12 @@ extern "C" {
 // SIZE_MAX then makes any allocation of it fail.
 constexpr uint64_t kMaxSegs = 1ull << 40;
 uint64_t seg_map_cap(uint64_t nseg) { return nseg < (1ull << 32) ? 4 * nseg + 65536 : 0; }
+// Test builds (MCK_QFAULT_TEST): MCHECKSUM_GPU_QFAULT_SCAN=b makes scan block
+// b give up its look-back (tests/test_gpu_fail_closed.py); ~0 = none.
+uint64_t scan_fault_block() {
+    const char *env = MCK_QFAULT_TEST ? getenv("MCHECKSUM_GPU_QFAULT_SCAN") : nullptr;
+    return env && env[0] ? strtoull(env, nullptr, 10) : ~0ull;
+}
 // scan blocks of a list (one at least: the scan launch writes the totals)
 uint64_t seg_blocks(uint64_t nseg) { return nseg ? (nseg + kScanBlk - 1) / kScanBlk : 1; }
 uint64_t seg_words(uint64_t nseg) { return 2 * (nseg + 1) + 2 + kDescWords * seg_blocks(nseg) + 3 * nseg; }
@@ -957,7 +979,7 @@ int mchecksum_gpu_checksum_segments(const char *hash_method, const uint64_t *dev
     hipError_t e = launch_kernel(seg_scan, dim3((unsigned)nb), dim3(kScanThreads), s, nullptr, dev_seg_len, dev_seg_addr,
                                  (uint64_t)nseg, desc, scan_epoch(), (uint64_t *)a.P, (uint64_t *)a.C,
                                  (unsigned long long *)a.ragged, dev_obj_first, (uint64_t)nobj, obj_w, (uint32_t *)a.map,
-                                 a.map_cap, dev_out, (uint32_t)width, preset, a.err_word);
+                                 a.map_cap, dev_out, (uint32_t)width, preset, a.err_word, scan_fault_block());
     if (e != hipSuccess) return hip_err(e, "segment scan launch");
     if (width == 32) {
         e = launch_kernel(seg_kernel<32, 0>, dim3(c->cus), dim3(1024), s, nullptr, a);

@@ -184,3 +184,36 @@ def test_product_library_reports_no_fault(gpu, batch):
         gpu.set_error_word(None)
     torch.cuda.synchronize()
     assert int(word.item()) == 0 and int(m.item()) == 0 and int(st.sum().item()) == 0
+
+
+def test_segment_scan_lookback_fault(gpu, qlib, monkeypatch):
+    """The one-launch segment scan's look-back in the fault-injecting build
+    (MCHECKSUM_GPU_QFAULT_SCAN=1: scan block 1 gives up its wait): the call
+    returns, nothing is read out of bounds (the chunk pass skips chunks whose
+    maps do not fit), and the caller's error word reports the failed scan --
+    whatever the outputs hold, they never read as verified."""
+    import torch
+    monkeypatch.setenv("MCHECKSUM_GPU_QFAULT_SCAN", "1")
+    nseg = 3000  # three scan blocks
+    data = torch.empty(nseg * 4096 + 64, dtype=torch.uint8, device="cuda")
+    gpu.fill_splitmix(data, 0x5CA1)
+    segs = [data[i * 4096:(i + 1) * 4096] for i in range(nseg)]
+    batch = gpu.SegmentBatch(segs, np.arange(0, nseg + 1, 3))
+    torch.cuda.synchronize()
+    word = torch.zeros(1, dtype=torch.int32, device="cuda")
+    n, base = batch.nseg, batch.meta.data_ptr()
+    out = torch.zeros(batch.nobj, dtype=torch.int64, device="cuda")
+    faults0 = qlib.mchecksum_gpu_queue_faults()
+    assert qlib.mchecksum_gpu_prepare(b"crc64") == 0
+    work = torch.empty((qlib.mchecksum_gpu_segments_work_size(n) + 7) // 8, dtype=torch.int64, device="cuda")
+    qlib.mchecksum_gpu_set_error_word(word.data_ptr())
+    try:
+        rc = qlib.mchecksum_gpu_checksum_segments(b"crc64", base, base + 8 * n, n, base + 16 * n, batch.nobj,
+                                                  work.data_ptr(), work.numel() * 8, out.data_ptr(),
+                                                  torch.cuda.current_stream().cuda_stream)
+    finally:
+        qlib.mchecksum_gpu_set_error_word(None)
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert int(word.item()) >= 1, "a scan whose look-back gave up must bump the error word"
+    assert qlib.mchecksum_gpu_queue_faults() - faults0 >= 1
