@@ -914,8 +914,12 @@ uint64_t seg_words(uint64_t nseg) { return 2 * (nseg + 1) + 2 + kDescWords * seg
 // reused memory, another) never match the current call's.
 uint64_t scan_epoch() {
     static std::atomic<uint64_t> ctr{[] {
-        std::random_device rd;
-        const uint64_t seed = ((uint64_t)rd() << 32 ^ rd() ^ (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count());
+        uint64_t seed = (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count() * 0x9E3779B97F4A7C15ull;
+        try {
+            std::random_device rd;
+            seed ^= (uint64_t)rd() << 32 ^ rd();
+        } catch (...) {  // no entropy source: the clock alone (never throw through the C ABI)
+        }
         return (seed & ((1ull << 60) - 1)) | 1ull;
     }()};
     return ctr.fetch_add(1, std::memory_order_relaxed) & ((1ull << 61) - 1);
