@@ -96,7 +96,7 @@ if [ "$P" = pmc ]; then
     timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/tr_${c}_f -o p -- python3 $R/tools/kernel_run.py --config $c --iters 4 > $O/tr_${c}_f.log 2>&1 || { tail $O/tr_${c}_f.log; exit 1; }
     timeout -k 10 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/tr_${c}_w -o p -- python3 $R/tools/kernel_run.py --config $c --iters 4 > $O/tr_${c}_w.log 2>&1 || { tail $O/tr_${c}_w.log; exit 1; }
     k=batch_kernel; pc=1; [ "$c" = xdr ] && k=xdr_fast_kernel
-    [ "$c" = seg ] && k=seg_ && pc=3  # scan reduce + scan down + chunk pass per call
+    [ "$c" = seg ] && k=seg_ && pc=2  # one-launch scan + chunk pass per call
     python3 $R/tools/pmc_traffic.py $O/tr_${c}_f $O/tr_${c}_w $k $O/pmc_traffic_$c.json $(python3 $R/tools/alg_bytes.py $c) $pc $((4 * pc)) || exit 1
   done
   cd "$R"
