@@ -1617,11 +1617,54 @@ __device__ __forceinline__ uint64_t hi64(uint4 v) { return (uint64_t)v.w << 32 |
 #ifndef MCK_RING64_NT
 #define MCK_RING64_NT MCK_RING64
 #endif
+// Whole rings (K a multiple of the ring, K >= 2 rings): no load or step is
+// conditional, so the waitcnt pass sees one load per step and waits
+// vmcnt(R - 1) throughout.  In the merged segment kernel the general loop
+// below -- conditional ring fill and tail -- kept only one or two loads in
+// flight (vmcnt(1) in its steady loop, vmcnt(0) after the fill): +2.5% on
+// seg for the even form (profiles/r04/ab_seg_even.log).  MCK_A64_EVEN=0: the
+// general loop for every K.
+#ifndef MCK_A64_EVEN
+#define MCK_A64_EVEN 1
+#endif
+template <int LOG2G, bool NT, bool OG>
+__device__ __forceinline__ uint64_t payload64_even(const uint8_t *lds, const crc64_gpu_pack_t *pk, const uint8_t *p,
+                                                   uint32_t K, uint32_t gl, uint32_t lc, uint64_t init) {
+    constexpr int G = 1 << LOG2G;
+    constexpr int R = NT ? MCK_RING64_NT : MCK_RING64;
+    Lane64 ln = lane64(lc);
+    gbyte_t src = global_ptr(p, LOG2G == 6) + 16u * gl;
+    uint4 ring[R];
+#pragma unroll
+    for (int u = 0; u < R; u++) ring[u] = ldg16<NT>(src + u * (16u * G));
+    // x holds state ^ (the data word of the step about to run)
+    uint64_t x0 = (gl == 0 ? init : 0ull) ^ lo64(ring[0]), x1 = hi64(ring[0]);
+    for (uint32_t k = R; k < K; k += R) {
+        src += R * (16u * G);
+#pragma unroll
+        for (int u = 0; u < R; u++) {
+            ring[u] = ldg16<NT>(src + u * (16u * G));
+            const uint4 nx = ring[(u + 1) % R];
+            x0 = f64x(lds, x0, lo64(nx), ln);
+            x1 = f64x(lds, x1, hi64(nx), ln);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < R; u++) {
+        const uint4 nx = u + 1 < R ? ring[u + 1] : make_uint4(0, 0, 0, 0);
+        x0 = f64x(lds, x0, lo64(nx), ln);
+        x1 = f64x(lds, x1, hi64(nx), ln);
+    }
+    return combine64<LOG2G, OG>(lds, pk, x0, x1, gl);
+}
+
 template <int LOG2G, bool NT, bool OG>
 __device__ __forceinline__ uint64_t payload64_aligned(const uint8_t *lds, const crc64_gpu_pack_t *pk, const uint8_t *p,
                                                       uint32_t K, uint32_t gl, uint32_t lc, uint64_t init) {
     constexpr int G = 1 << LOG2G;
     constexpr int R = NT ? MCK_RING64_NT : MCK_RING64;
+    if (MCK_A64_EVEN && MCK_LA64 && K % R == 0 && K >= 2 * R)
+        return payload64_even<LOG2G, NT, OG>(lds, pk, p, K, gl, lc, init);
     Lane64 ln = lane64(lc);
     // global (address-space 1) loads: a flat load would also hold up every LDS wait
     const gbyte_t src = global_ptr(p, LOG2G == 6) + 16u * gl;

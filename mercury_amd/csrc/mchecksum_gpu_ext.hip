@@ -68,9 +68,10 @@ struct SegArgs {
     const uint64_t *P, *C;  // workspace: byte / chunk exclusive prefix sums, nseg + 1 each
     const unsigned long long *ragged;  // workspace: non-zero if any chunk needs the ragged loop
     // workspace: per segment s, {its object j (kNoObj outside [first[0],
-    // first[nobj])), first[j], first[j + 1]} (3 words: the queue pass finds a
-    // chunk's object bounds in one round of loads), and the segment of each
-    // chunk while the chunks fit map_cap
+    // first[nobj])), first[j], first[j + 1], the object's head segment (its
+    // first non-empty one; kNoObj when the scan block could not tell)} (4
+    // words: one scalar load in the queue pass), and the segment of each chunk
+    // while the chunks fit map_cap
     const uint64_t *obj;
     const uint32_t *map;
     uint64_t map_cap;
@@ -316,18 +317,33 @@ __global__ __launch_bounds__(kScanThreads) void seg_scan(const uint64_t *len, co
     uint64_t ep = ex[0] + p - p0, ec = ex[1] + c - c0;
     __shared__ uint64_t row[kScanBlk];
     __shared__ uint64_t row_f0[kScanBlk], row_f1[kScanBlk];  // the object's first[j], first[j + 1]
+    __shared__ uint64_t row_hs[kScanBlk];                      // the object's head segment
+    __shared__ uint32_t row_ne[kScanBlk];                      // 1: the segment is not empty
     if (obj) {
         for (uint32_t t = threadIdx.x; t < kScanBlk; t += kScanThreads) row[t] = kNoObj;
+#pragma unroll
+        for (uint32_t e = 0; e < kScanPer; e++) row_ne[threadIdx.x * kScanPer + e] = l[e] != 0;
         __syncthreads();
         if (lo_s < hi_s) {
             const uint64_t jb = jb_s, je = je_s;
             for (uint64_t k = jb + threadIdx.x; k <= je; k += kScanThreads) {
                 const uint64_t a0 = first[k], a1 = first[k + 1];
                 const uint64_t lo = a0 > lo_s ? a0 : lo_s, hi = a1 < hi_s ? a1 : hi_s;
+                // the head segment is known here when the object starts in this
+                // block and one of its segments here is not empty; otherwise
+                // (kNoObj) the chunk pass compares byte offsets instead
+                uint64_t hs = kNoObj;
+                if (a0 >= s0)
+                    for (uint64_t i = lo; i < hi; i++)
+                        if (row_ne[i - s0]) {
+                            hs = i;
+                            break;
+                        }
                 for (uint64_t i = lo; i < hi; i++) {
                     row[i - s0] = k;
                     row_f0[i - s0] = a0;
                     row_f1[i - s0] = a1;
+                    row_hs[i - s0] = hs;
                 }
             }
         }
@@ -341,10 +357,11 @@ __global__ __launch_bounds__(kScanThreads) void seg_scan(const uint64_t *len, co
             C[i] = ec;
             if (obj) {
                 const uint64_t t = i - s0;
-                obj[3 * i] = row[t];
+                obj[4 * i] = row[t];
                 if (row[t] != kNoObj) {
-                    obj[3 * i + 1] = row_f0[t];
-                    obj[3 * i + 2] = row_f1[t];
+                    obj[4 * i + 1] = row_f0[t];
+                    obj[4 * i + 2] = row_f1[t];
+                    obj[4 * i + 3] = row_hs[t];
                 }
             }
             // chunk -> segment map, while it fits (the chunk passes check the
@@ -382,9 +399,10 @@ struct ChunkWalk {
     }
 
     // Next chunk: its bytes [addr, addr + n) and, when its segment belongs to
-    // an object (*in), the object, the object bytes that follow it and
-    // whether it starts the object (*head).
-    __device__ bool next(uint64_t *addr, uint64_t *n, bool *in, uint64_t *obj, uint64_t *after, bool *head) {
+    // an object (*in), the object, the object bytes that follow it (*end -
+    // *stop, as seg_locate) and whether it starts the object (*head).
+    __device__ bool next(uint64_t *addr, uint64_t *n, bool *in, uint64_t *obj, uint64_t *end, uint64_t *stop,
+                         bool *head) {
         if (c >= c1) return false;
         while (s < a->nseg && a->C[s + 1] <= c) s++;  // skips empty segments
         const uint64_t cs = s < a->nseg ? a->C[s] : ~0ull, L = s < a->nseg ? a->len[s] : 0;
@@ -400,7 +418,8 @@ struct ChunkWalk {
         if (*in) {
             while (j + 1 < a->nobj && a->first[j + 1] <= s) j++;
             *obj = j;
-            *after = a->P[a->first[j + 1]] - (a->P[s] + off + *n);
+            *end = a->P[a->first[j + 1]];
+            *stop = a->P[s] + off + *n;
             *head = a->P[s] + off == a->P[a->first[j]];
         }
         c++;
@@ -423,12 +442,25 @@ struct ChunkWalk {
 #endif
 
 // Chunk c (< nchunks): its bytes [addr, addr + n) and, when its segment
-// belongs to an object (*in), the object, the object bytes after it and
-// whether it starts the object (*head).  c is wave-uniform, so every load is
-// scalar.
+// belongs to an object (*in), the object, the object bytes after it (*end -
+// *stop) and whether it starts the object (*head).  c is wave-uniform, so
+// every load is scalar: the map, then the segment's words and its 4-word
+// object record.  The object's end offset (*end) is a third dependent load,
+// but the payload loop does not wait for it -- the caller subtracts only
+// after the loop (round 4: the head test from the record's head segment
+// instead of the object's start offset, a second third-round load).  Only a
+// chunk whose object's head the scan block could not place compares byte
+// offsets.  Locate latency is not what limits the pass: two rounds instead
+// of three measured within noise, and so did a one-round locate of bench.py's
+// seg layout from the chunk index alone; the same layout with a constant
+// chunk length measured +1.6-2.5% -- the compile-time trip count gave the
+// payload loop whole-ring code (payload64_even, crc_gpu_device.h), now taken
+// for every chunk of whole rings (profiles/r04/ab_seg_locate_bound.log,
+// ab_seg_cheats.log, ab_seg_full.log, ab_seg_head.log, ab_seg_even.log).
 __device__ __forceinline__ __attribute__((unused)) void seg_locate(const SegArgs &a, uint64_t c, uint64_t nchunks,
                                                                    uint64_t *addr, uint64_t *n, bool *in,
-                                                                   uint64_t *obj, uint64_t *after, bool *head) {
+                                                                   uint64_t *obj, uint64_t *end, uint64_t *stop,
+                                                                   bool *head) {
     const uint64_t s = nchunks <= a.map_cap ? (uint64_t)a.map[c] : lower_bound_u64(a.C, a.nseg + 1, c + 1) - 1;
     // (a scan whose look-back gave up -- reported on the error word -- leaves
     // maps that may not fit: such a chunk is skipped, never read out of bounds)
@@ -440,14 +472,16 @@ __device__ __forceinline__ __attribute__((unused)) void seg_locate(const SegArgs
     }
     *addr = a.addr[s] + off;
     *n = L - off < kChunk ? L - off : kChunk;
-    const uint64_t *o3 = a.obj + 3 * s;  // {j, first[j], first[j + 1]}
-    const uint64_t j = o3[0];
+    const uint64_t *o4 = a.obj + 4 * s;  // {j, first[j], first[j + 1], head segment}
+    const uint64_t j = o4[0];
     *in = j != kNoObj;
     if (*in) {
         *obj = j;
         const uint64_t at = a.P[s] + off;
-        *after = a.P[o3[2]] - (at + *n);
-        *head = at == a.P[o3[1]];
+        *end = a.P[o4[2]];
+        *stop = at + *n;
+        const uint64_t hs = o4[3];
+        *head = hs != kNoObj ? hs == s && off == 0 : at == a.P[o4[1]];
     }
 }
 
@@ -483,23 +517,23 @@ __global__ __launch_bounds__(1024, kSegWavesPerEU<W * 4 + PART>) void seg_kernel
     constexpr bool kQueue = MCK_SEG_QUEUE && (PART == 1 || PART == 3);
     __shared__ WgQueue wgq;
     if (kQueue && threadIdx.x == 0) wg_queue_init(&wgq, a.queue, nchunks);
-    // Calls body(addr, n, j, after, head) for every chunk of this wave that
+    // Calls body(addr, n, j, end, stop, head) for every chunk of this wave that
     // belongs to an object; true in the first wave of a launch whose queue
     // wait gave up (the caller's error word then gets +1: fail closed).
     auto chunks = [&](auto &&body) -> bool {
         if constexpr (kQueue) {
             return for_each_unit<true>(&wgq, a.queue, nchunks, wave, nw, [&](uint64_t c) {
-                uint64_t p, n, j = 0, after = 0;
+                uint64_t p, n, j = 0, end = 0, stop = 0;
                 bool in, head = false;
-                seg_locate(a, c, nchunks, &p, &n, &in, &j, &after, &head);
-                if (in) body(p, n, j, after, head);
+                seg_locate(a, c, nchunks, &p, &n, &in, &j, &end, &stop, &head);
+                if (in) body(p, n, j, end, stop, head);
             });
         } else {
             ChunkWalk walk(a, wave, nw, nchunks);
-            uint64_t p, n, j = 0, after = 0;
+            uint64_t p, n, j = 0, end = 0, stop = 0;
             bool in, head = false;
-            while (walk.next(&p, &n, &in, &j, &after, &head))
-                if (in) body(p, n, j, after, head);
+            while (walk.next(&p, &n, &in, &j, &end, &stop, &head))
+                if (in) body(p, n, j, end, stop, head);
             return false;
         }
     };
@@ -514,7 +548,7 @@ __global__ __launch_bounds__(1024, kSegWavesPerEU<W * 4 + PART>) void seg_kernel
         uint32_t *out = reinterpret_cast<uint32_t *>(a.out);
         const bool nt = uniform(a.P[a.nseg]) >= kSegNtBytes;  // as for CRC-64 below
         const uint32_t init = pk->init;
-        const bool faulted = chunks([&](uint64_t p, uint64_t n, uint64_t j, uint64_t after, bool head) {
+        const bool faulted = chunks([&](uint64_t p, uint64_t n, uint64_t j, uint64_t end, uint64_t stop, bool head) {
             const uint8_t *q = reinterpret_cast<const uint8_t *>(p);
             // whole rings of 1 KiB steps from a 16-B aligned start (the usual
             // bulk segment) take the aligned loop: no edge masks, no pad operator
@@ -527,7 +561,7 @@ __global__ __launch_bounds__(1024, kSegWavesPerEU<W * 4 + PART>) void seg_kernel
                                           : payload32_g64<false, Tab32<false>, true>(lds, pk, q, n, lane, lc0, lc1, reg);
             x = uniform(x);
             if (head && n < 4) x ^= pk->zinit[n];
-            x = shift32(sp, x, after);
+            x = shift32(sp, x, end - stop);  // (the object bytes after the chunk)
             if (lane == 0) atomicXor(out + j, head ? x ^ init : x);  // ^ init: cancels the preset's
         });
         if (faulted && lane == 0 && a.err_word) atomicAdd(a.err_word, 1u);
@@ -549,7 +583,7 @@ __global__ __launch_bounds__(1024, kSegWavesPerEU<W * 4 + PART>) void seg_kernel
         // branch measured the same and spills more).
         [[maybe_unused]] const bool nt = uniform(a.P[a.nseg]) >= kSegNtBytes;
         const uint64_t init = pk->init;
-        const bool faulted = chunks([&](uint64_t p, uint64_t n, uint64_t j, uint64_t after, bool head) {
+        const bool faulted = chunks([&](uint64_t p, uint64_t n, uint64_t j, uint64_t end, uint64_t stop, bool head) {
             const uint8_t *q = reinterpret_cast<const uint8_t *>(p);
             const bool aligned = p % 16 == 0 && n % 1024 == 0;
             if (PART != 3 && aligned != (PART == 1)) return;
@@ -564,7 +598,7 @@ __global__ __launch_bounds__(1024, kSegWavesPerEU<W * 4 + PART>) void seg_kernel
                 x = payload64_g64<false, true>(lds, pk, q, n, lane, lc, reg);
             x = uniform(x);
             if (!aligned && head && n < 8) x ^= pk->zinit[n];
-            x = shift64(sp, x, after);
+            x = shift64(sp, x, end - stop);  // (the object bytes after the chunk)
             if (lane == 0) atomicXor(out + j, (unsigned long long)(head ? x ^ init : x));  // ^ init: cancels the preset's
         });
         if (faulted && lane == 0 && a.err_word) atomicAdd(a.err_word, 1u);
@@ -893,7 +927,7 @@ extern "C" {
 
 // P, C (nseg + 1 each), the ragged flag (+ pad), the look-back descriptor of
 // each scan block (kDescWords), each segment's object and its bounds in
-// first[] (3 nseg), then the chunk -> segment map (u32 entries:
+// first[] and its head segment (4 nseg), then the chunk -> segment map (u32 entries:
 // 4 per segment + 64 Ki, i.e. lists averaging up to ~1 MiB per segment, or
 // one huge segment up to 16 GiB; none past 2^32 segments).  More than 2^40
 // segments (far beyond device memory) is rejected, so the size cannot wrap:
@@ -908,7 +942,7 @@ uint64_t scan_fault_block() {
 }
 // scan blocks of a list (one at least: the scan launch writes the totals)
 uint64_t seg_blocks(uint64_t nseg) { return nseg ? (nseg + kScanBlk - 1) / kScanBlk : 1; }
-uint64_t seg_words(uint64_t nseg) { return 2 * (nseg + 1) + 2 + kDescWords * seg_blocks(nseg) + 3 * nseg; }
+uint64_t seg_words(uint64_t nseg) { return 2 * (nseg + 1) + 2 + kDescWords * seg_blocks(nseg) + 4 * nseg; }
 // The scan's look-back epochs: a process-wide counter from a random seed, so a
 // workspace's descriptors from any earlier call (this process or, through
 // reused memory, another) never match the current call's.

@@ -90,11 +90,11 @@ def test_batch_arguments_rejected_before_any_device_work(product_lib):
     ]
     ws = L.mchecksum_gpu_segments_work_size
     ws.restype = ctypes.c_size_t
-    # P, C, flag, per scan block a look-back descriptor (8), segment -> (object, its first[] bounds) (u64 words), then the
+    # P, C, flag, per scan block a look-back descriptor (8), segment -> (object, its first[] bounds, its head segment) (u64 words), then the
     # chunk -> segment map (u32, 4 per segment + 64 Ki; none past 2^32 segments)
-    assert ws(4) == 8 * (2 * 5 + 2 + 8 + 3 * 4) + 4 * (4 * 4 + 65536) and ws((1 << 40) + 1) == (1 << 64) - 1
+    assert ws(4) == 8 * (2 * 5 + 2 + 8 + 4 * 4) + 4 * (4 * 4 + 65536) and ws((1 << 40) + 1) == (1 << 64) - 1
     n = 1 << 32
-    assert ws(n) == 8 * (2 * (n + 1) + 2 + 8 * (n // 1024) + 3 * n)
+    assert ws(n) == 8 * (2 * (n + 1) + 2 + 8 * (n // 1024) + 4 * n)
     first = (ctypes.c_uint64 * 2)(0, 1)
     cases += [
         (lambda: L.mchecksum_gpu_checksum_segments(b"crc64", offs, offs, 1, first, 1, buf, 8, buf, None), "workspace"),

@@ -255,6 +255,33 @@ def test_segments_long_lists_multi_block_scan(gpu, buf, oracle_mod, method, layo
     assert got.tolist() == _want(oracle_mod, method, host, segs, first)
 
 
+@pytest.mark.parametrize("method", ["crc32c", "crc64", "crc64-ecma182"])
+def test_segments_leading_empty_segments_across_scan_blocks(gpu, buf, oracle_mod, method):
+    """The object's head chunk (the one that starts from the register init):
+    the scan records each object's first non-empty segment when the object
+    starts in the same 1024-segment scan block; objects that start in an
+    earlier block fall back to comparing byte offsets.  Heads after leading
+    empty segments -- inside the block, in the next block, two blocks on --
+    and multi-chunk head segments (only their first chunk is the head)."""
+    host = _host(buf)
+    rng = np.random.default_rng(2024)
+    n = 3200
+    lens = [int(x) for x in rng.integers(1, 300, n)]
+    for s in range(1000, 1024):   # object A = [1000, 1030): head in block 1
+        lens[s] = 0
+    for s in range(1030, 2053):   # object B = [1030, 2100): head two blocks on
+        lens[s] = 0
+    lens[2053] = 600000           # a 3-chunk head segment
+    lens[10] = lens[11] = 0       # object [10, 20): head inside block 0
+    lens[12] = (256 << 10) + 7
+    lens[3070] = lens[3071] = 0   # object [3070, 3080): starts and heads in block 2
+    offs = [int(o) for o in rng.integers(0, buf.numel() - 600064, n)]
+    segs = list(zip(offs, lens))
+    first = sorted(set([0, 10, 20, 500, 1000, 1030, 2100, 2500, 3070, 3080, n]))
+    got = gpu.as_unsigned(gpu.checksum_segments(method, [buf[o:o + ln] for o, ln in segs], first))
+    assert got.tolist() == _want(oracle_mod, method, host, segs, first)
+
+
 @pytest.mark.parametrize("method", ["crc32c", "crc64"])
 def test_segments_large_batch_non_temporal(gpu, buf, oracle_mod, method):
     """>= 512 MiB in one call takes the non-temporal loads (decided on the
