@@ -192,9 +192,14 @@ struct BatchArgs {
     // MSB-first model on a verify call: the kernel's value is the CRC
     // byte-swapped (crc_gpu_layout.h), so swap before comparing
     uint32_t bswap;
+    // split CRC-64: 1 = every queue chunk holds whole payloads (split_chunks_whole),
+    // so the pieces combine in the workgroup's LDS and out[] needs no zeroing
+    uint32_t split_lds;
 };
 // Piece size of a split payload: 256 KiB = 256 steps of the G = 64 loop.
 constexpr uint64_t kSplitBytes = 256u << 10;
+// Payloads per queue chunk whose pieces a workgroup can combine in LDS.
+constexpr uint32_t kSplitAcc = 16;
 
 // ------------------------------------------------------------ work queue --
 // Dynamic distribution of payloads over waves.  With a static assignment the
@@ -324,6 +329,16 @@ struct ChunkPlan {
     }
     __device__ __forceinline__ uint32_t size(uint64_t id) const { return id < nbig ? 1u << cl : 1u << sl; }
 };
+// Split CRC-64: does every queue chunk of `units` pieces (`pieces` per payload,
+// a power of two) on `grid` workgroups hold whole payloads, at most kSplitAcc
+// of them?  (ChunkPlan's sizes; chunk starts are multiples of the tail size.)
+__host__ __device__ inline bool split_chunks_whole(uint64_t units, uint32_t grid, uint32_t pieces) {
+    const uint64_t share = units / (4ull * grid);
+    uint32_t cl = 0;
+    while (cl < kWgChunkMaxLog2 && (2ull << cl) <= share) cl++;
+    const uint32_t sl = MCK_QTAIL && cl >= MCK_QTAIL_SHIFT ? cl - MCK_QTAIL_SHIFT : cl;
+    return pieces >= 2 && pieces <= (1u << sl) && (1u << cl) / pieces <= kSplitAcc;
+}
 constexpr uint32_t kWgRing = 8;    // LDS ring of published chunk ids
 constexpr uint64_t kNoChunk = 0xFFFFFFFFull;
 
@@ -513,7 +528,11 @@ __device__ __forceinline__ T wave_max(T v) {
 // q0 = min(n, nw) -- wg_queue_init gets n - q0 (first_static_units).
 __device__ __forceinline__ uint64_t first_static_units(uint64_t n, uint32_t nw) { return n < nw ? n : nw; }
 
-template <bool DYN, bool FIRST = false, class F>
+// DEFER (the split CRC-64 kernel's in-workgroup combine): body(u, r) gets
+// its chunk's ring entry r, and a taker counts itself a reader of the entry
+// only once body has returned -- the entry is not republished while any of
+// its units runs, so per-entry state in LDS outlives them all.
+template <bool DYN, bool FIRST = false, bool DEFER = false, class F>
 __device__ __forceinline__ bool for_each_unit(WgQueue *L, unsigned long long *queue, uint64_t n, uint32_t wave,
                                               uint32_t nw, F &&body) {
     if constexpr (DYN) {
@@ -538,6 +557,8 @@ __device__ __forceinline__ bool for_each_unit(WgQueue *L, unsigned long long *qu
         uint32_t flt = 0;  // lane 0: a wait of this wave gave up
         for (;;) {
             uint64_t u;
+            uint32_t rr = 0, dfr = 0;  // DEFER: the unit's ring entry; lane 0: its read is still to count
+            (void)rr;
             if (__builtin_amdgcn_readfirstlane(lds_ld(&L->busy))) {
                 if (su >= n) break;
                 u = su;
@@ -572,7 +593,7 @@ __device__ __forceinline__ bool for_each_unit(WgQueue *L, unsigned long long *qu
                         e = kNoChunk;
                         flt = 1;
                     }
-                    atomicAdd(&L->reads[r], 1u);
+                    if constexpr (!DEFER) atomicAdd(&L->reads[r], 1u);
                     // One taker per chunk (slot cu - lead) fetches the next
                     // chunk -- after its own chunk is known, so fetches run in
                     // chunk order and the first kNoChunk is final.
@@ -599,6 +620,11 @@ __device__ __forceinline__ bool for_each_unit(WgQueue *L, unsigned long long *qu
                         flt = 1;
                     }
 #endif
+                    if constexpr (DEFER) {  // a unit's read counts after its body; a skipped slot's now
+                        const uint64_t id0 = e & 0xFFFFFFFFull;
+                        dfr = id0 != kNoChunk && (t & (cu - 1)) < plan.size(id0);
+                        if (!dfr) atomicAdd(&L->reads[r], 1u);
+                    }
                 }
                 t = __builtin_amdgcn_readfirstlane(t);
                 const uint64_t id = uniform64(e) & 0xFFFFFFFFull;
@@ -606,11 +632,17 @@ __device__ __forceinline__ bool for_each_unit(WgQueue *L, unsigned long long *qu
                 // every chunk spans cu slots; a tail chunk's slots past its size are skipped
                 const uint32_t k = t & (cu - 1);
                 u = k < plan.size(id) ? q0 + plan.start(id) + k : n;
+                rr = (t >> cl) % kWgRing;
             }
 #if MCK_TRACE
             const unsigned long long b0 = wall_clock64();
 #endif
-            if (u < n) body(u);
+            if constexpr (DEFER) {
+                if (u < n) body(u, rr);
+                if (l0 && dfr) __hip_atomic_fetch_add(&L->reads[rr], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            } else {
+                if (u < n) body(u);
+            }
 #if MCK_TRACE
             qs_busy += wall_clock64() - b0;
             qs_units += u < n;
@@ -634,7 +666,10 @@ __device__ __forceinline__ bool for_each_unit(WgQueue *L, unsigned long long *qu
         (void)nw;
         return __builtin_amdgcn_readfirstlane(first) != 0;
     } else {
-        for (uint64_t u = FIRST ? (uint64_t)wave + nw : wave; u < n; u += nw) body(u);
+        for (uint64_t u = FIRST ? (uint64_t)wave + nw : wave; u < n; u += nw) {
+            if constexpr (DEFER) body(u, 0u);
+            else body(u);
+        }
         return false;
     }
 }
@@ -1860,6 +1895,13 @@ __global__ __launch_bounds__(kBlk64<MODE>, kWpe64<MODE>) void crc64_batch_kernel
     constexpr bool DYN = dyn_policy(64, MODE, NT, false) || SPLIT;
     MCK_STAMP(blockIdx.x * kWPB + (threadIdx.x >> 6), 0);
     if (DYN && threadIdx.x == 0) wg_queue_init(&wgq, a.queue, units);
+    // split pieces combined in the workgroup (SPLIT, split_lds)
+    __shared__ unsigned long long sacc[SPLIT ? kWgRing * kSplitAcc : 1];
+    __shared__ unsigned int scnt[SPLIT ? kWgRing * kSplitAcc : 1];
+    if (SPLIT && threadIdx.x < kWgRing * kSplitAcc) {
+        sacc[threadIdx.x] = 0;
+        scnt[threadIdx.x] = 0;
+    }
     fill_lds64<S::block, S::ops_mode>(lds, pk);
     __syncthreads();
     MCK_STAMP(blockIdx.x * kWPB + (threadIdx.x >> 6), 1);
@@ -1892,17 +1934,41 @@ __global__ __launch_bounds__(kBlk64<MODE>, kWpe64<MODE>) void crc64_batch_kernel
         static_assert(LOG2G == 6 && MODE == kFixedAligned && !VERIFY, "split pieces: aligned G = 64 checksums");
         const uint32_t sl = a.split_log2, pieces = 1u << sl;
         const crc64_shift_pack_t *sp = reinterpret_cast<const crc64_shift_pack_t *>(a.shift);
-        const bool faulted = for_each_unit<true>(&wgq, a.queue, units, wave, nw, [&](uint64_t u) {
-            const uint64_t p = u >> sl;
-            const uint32_t q = (uint32_t)u & (pieces - 1);
-            const uint64_t x = payload64_aligned<6, NT, S::ops_global>(
-                lds, pk, a.base + p * a.stride + (uint64_t)q * kSplitBytes, (uint32_t)(kSplitBytes >> 10), gl, lc,
-                q == 0 ? pk->init : 0ull);
-            if (gl == 0) {
-                const uint64_t t = shift64(sp, x, (uint64_t)(pieces - 1 - q) * kSplitBytes) ^ (q == 0 ? xorout : 0ull);
-                atomicXor(reinterpret_cast<unsigned long long *>(a.out) + p, (unsigned long long)t);
-            }
-        });
+        unsigned long long *out = reinterpret_cast<unsigned long long *>(a.out);
+        // In-workgroup combine (split_lds, a slot launch whose queue chunks hold
+        // whole payloads): per ring entry and payload, the XOR of the pieces'
+        // terms and their count; the last piece stores the CRC -- no zeroing
+        // launch and no global atomics.  Otherwise (graph captures: static
+        // split) each piece XORs its term into the out[] the host zeroed.
+        // (The host's check is repeated here: a mismatch is a fault, never a
+        // silently wrong value.)
+        const bool in_wg = a.split_lds && a.queue && split_chunks_whole(units, gridDim.x, pieces);
+        bool faulted = a.split_lds && !in_wg;
+        if (faulted && threadIdx.x == 0) queue_fault(13, units, pieces);
+        if (!faulted)
+            faulted = for_each_unit<true, false, true>(&wgq, a.queue, units, wave, nw, [&](uint64_t u, uint32_t r) {
+                const uint64_t p = u >> sl;
+                const uint32_t q = (uint32_t)u & (pieces - 1);
+                const uint64_t x = payload64_aligned<6, NT, S::ops_global>(
+                    lds, pk, a.base + p * a.stride + (uint64_t)q * kSplitBytes, (uint32_t)(kSplitBytes >> 10), gl, lc,
+                    q == 0 ? pk->init : 0ull);
+                if (gl == 0) {
+                    const uint64_t t = shift64(sp, x, (uint64_t)(pieces - 1 - q) * kSplitBytes) ^ (q == 0 ? xorout : 0ull);
+                    if (in_wg) {
+                        // (one wave's LDS atomics are performed in order: a piece's
+                        // XOR lands before its count)
+                        const uint32_t ai = r * kSplitAcc + (uint32_t)(p & (kSplitAcc - 1));
+                        __hip_atomic_fetch_xor(&sacc[ai], (unsigned long long)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        const uint32_t seen = __hip_atomic_fetch_add(&scnt[ai], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        if (seen == pieces - 1) {
+                            out[p] = __hip_atomic_exchange(&sacc[ai], 0ull, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            __hip_atomic_store(&scnt[ai], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        }
+                    } else {
+                        atomicXor(out + p, (unsigned long long)t);
+                    }
+                }
+            });
         if (faulted) fail_closed<false>(a);
         return;
     }

@@ -487,6 +487,13 @@ bool use_split(int width, int lg, bool aligned, bool nt, size_t len, size_t stri
     return MCK_SPLIT64 && shape && nt;
 }
 
+// MCHECKSUM_GPU_SPLIT_LDS=0: split CRC-64 pieces always combine through the
+// zeroed output (tests, A/B).
+bool use_split_lds() {
+    const char *env = getenv("MCHECKSUM_GPU_SPLIT_LDS");
+    return !(env && env[0] == '0');
+}
+
 int launch_fixed(DevCtx *c, int idx, const void *pack, int width, int lg, const void *dev_base, size_t stride,
                  size_t len, size_t count, void *dev_out, void *stream, bool light) {
     const uint64_t step = 16ull << lg;
@@ -514,15 +521,6 @@ int launch_fixed(DevCtx *c, int idx, const void *pack, int width, int lg, const 
         }
         a.shift = shift;
         a.split_log2 = sl;
-        // the pieces XOR their terms into out[]: zero it first, in stream order,
-        // with a kernel -- a hipMemsetAsync captured into a graph did not order
-        // against the kernel node on replays after the first (the pieces landed
-        // in a half-zeroed output: tests/test_gpu_queue.py, concurrent replays)
-        uint64_t zb = (count + 255) / 256;
-        zb = zb > 1024 ? 1024 : zb;
-        const hipError_t e = launch_kernel(zero_u64_kernel, dim3((unsigned)zb), dim3(256), (hipStream_t)stream, nullptr,
-                                           reinterpret_cast<unsigned long long *>(dev_out), (uint64_t)count);
-        if (e != hipSuccess) return hip_err(e, "output zeroing");
         const KLaunch k = nt ? KLaunch{crc64_batch_kernel<6, kFixedAligned, false, true, true>, Shape<64, kFixedAligned>::block,
                                        Shape<64, kFixedAligned>::blocks_per_cu}
                              : KLaunch{crc64_batch_kernel<6, kFixedAligned, false, false, true>, Shape<64, kFixedAligned>::block,
@@ -530,6 +528,23 @@ int launch_fixed(DevCtx *c, int idx, const void *pack, int width, int lg, const 
         const unsigned grid = grid_for(c, (uint64_t)count << sl, k);
         SlotRef sr = queue_slot(c, stream);
         a.queue = sr.q;
+        // With a slot and queue chunks of whole payloads the pieces combine in
+        // their workgroup (crc_gpu_device.h, split_lds).  Otherwise they XOR
+        // their terms into out[]: zero it first, in stream order, with a kernel
+        // -- a hipMemsetAsync captured into a graph did not order against the
+        // kernel node on replays after the first (the pieces landed in a
+        // half-zeroed output: tests/test_gpu_queue.py, concurrent replays).
+        a.split_lds = sr.q && use_split_lds() && split_chunks_whole((uint64_t)count << sl, grid, 1u << sl) ? 1u : 0u;
+        if (!a.split_lds) {
+            uint64_t zb = (count + 255) / 256;
+            zb = zb > 1024 ? 1024 : zb;
+            const hipError_t e = launch_kernel(zero_u64_kernel, dim3((unsigned)zb), dim3(256), (hipStream_t)stream, nullptr,
+                                               reinterpret_cast<unsigned long long *>(dev_out), (uint64_t)count);
+            if (e != hipSuccess) {
+                slot_unissue(c, sr);
+                return hip_err(e, "output zeroing");
+            }
+        }
         int rc = launch(c, k, a, grid, stream, sr);
         if (rc == MCHECKSUM_GPU_OK && gpu_msb(idx)) rc = swap_outputs(dev_out, count, width, stream);
         return rc;
