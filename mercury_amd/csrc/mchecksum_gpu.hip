@@ -305,13 +305,24 @@ struct KLaunch {
     int block, blocks_per_cu;
 };
 
-int choose_log2g(size_t len) {
+int choose_log2g(size_t len, int width) {
     const char *env = getenv("MCHECKSUM_GPU_LOG2G");
     if (env && env[0]) {
         const int v = atoi(env);
         if (v >= 0 && v <= CRC_GPU_MAX_LOG2G) return v;
     }
-    // Aim for >= 16 steps per payload, at most 64 lanes per payload.
+    // CRC-32 (round 4, one-process sweeps of 2..64 lanes over 1-16 KiB
+    // payloads, profiles/r04/ab_fixed_log2g*.log): 4 lanes from 1 KiB to under
+    // 8 KiB (C2's 4 KiB -1.9%, 2 KiB -1.4% against 8 and 16 lanes), then
+    // about 32 steps per payload (8 KiB: 16 lanes -1.2%, 16 KiB: 32 lanes
+    // -5.6%, against 32 and 64); 64 lanes from 32 KiB (the headline).
+    if (width == 32 && len >= 1024) {
+        if (len < 8192) return 2;
+        int lg = 0;
+        while (lg < CRC_GPU_MAX_LOG2G && ((size_t)512 << (lg + 1)) <= len) lg++;
+        return lg;
+    }
+    // Otherwise aim for >= 16 steps per payload, at most 64 lanes per payload.
     const size_t target = len / 256;
     int lg = 0;
     while (lg < CRC_GPU_MAX_LOG2G && ((size_t)1 << (lg + 1)) <= target) lg++;
@@ -617,7 +628,7 @@ int mchecksum_gpu_prepare(const char *hash_method) {
 int mchecksum_gpu_lanes_per_payload(const char *hash_method, size_t len) {
     int width = 0;
     if (gpu_model(hash_method, &width) < 0) return -1;
-    return 1 << choose_log2g(len);
+    return 1 << choose_log2g(len, width);
 }
 
 int mchecksum_gpu_checksum_fixed(const char *hash_method, const void *dev_base, size_t stride, size_t len,
@@ -640,7 +651,7 @@ int mchecksum_gpu_checksum_fixed(const char *hash_method, const void *dev_base, 
         return launch_fixed(c, gpu_model(hash_method, &width), pack, width, lg, dev_base, stride, len, count, dev_out,
                             stream, true);
     }
-    const int lg = choose_log2g(len);
+    const int lg = choose_log2g(len, width);
     DevCtx *c = nullptr;
     const void *pack = nullptr;
     int rc = prologue(hash_method, lg, &width, &c, &pack);

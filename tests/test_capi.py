@@ -116,7 +116,10 @@ def test_batch_arguments_rejected_before_any_device_work(product_lib):
 def test_lanes_per_payload_heuristic(product_lib):
     f = product_lib.mchecksum_gpu_lanes_per_payload
     assert f(b"crc32c", 65536) == 64
-    assert f(b"crc32c", 4096) == 16
+    # CRC-32 (round-4 sweeps): 4 lanes from 1 KiB to under 8 KiB, then ~32 steps per payload
+    assert [f(b"crc32c", n) for n in (1024, 2048, 4096, 6144, 8192, 16384, 32768)] == [4, 4, 4, 4, 16, 32, 64]
+    assert f(b"crc32c", 512) == 2
+    assert f(b"crc64", 4096) == 16  # CRC-64 keeps >= 16 steps per payload
     assert f(b"crc64", 1 << 20) == 64
     assert f(b"crc32c", 64) == 1
     assert f(b"crc16", 4096) == -1  # crc16 has no GPU kernel (CPU header path only)

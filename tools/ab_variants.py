@@ -22,6 +22,11 @@ from mercury_amd import gpu as G  # noqa: E402
 SHAPES = {
     "metric": ("crc32c", 65536, 65536, 0x4D43310000000005),
     "c2": ("crc32c", 65536, 4096, 0x4D43310000000002),
+    # lanes-per-payload policy (choose_log2g) checks: other fixed payload sizes
+    "f1k": ("crc32c", 262144, 1024, 0x4D43310000000002),
+    "f2k": ("crc32c", 131072, 2048, 0x4D43310000000002),
+    "f8k": ("crc32c", 65536, 8192, 0x4D43310000000002),
+    "f16k": ("crc32c", 65536, 16384, 0x4D43310000000002),
     "c3": ("crc64", 8192, 1 << 20, 0x4D43310000000003),
     "c4": ("crc32c", 262144, None, 0x4D43310000000004),   # offsets table, U[64 B, 64 KiB]
     "c4_64": ("crc64", 262144, None, 0x4D43310000000004),
