@@ -119,7 +119,8 @@ def test_lanes_per_payload_heuristic(product_lib):
     # CRC-32 (round-4 sweeps): 4 lanes from 1 KiB to under 8 KiB, then ~32 steps per payload
     assert [f(b"crc32c", n) for n in (1024, 2048, 4096, 6144, 8192, 16384, 32768)] == [4, 4, 4, 4, 16, 32, 64]
     assert f(b"crc32c", 512) == 2
-    assert f(b"crc64", 4096) == 16  # CRC-64 keeps >= 16 steps per payload
+    # CRC-64: about 128 steps per payload, 4 lanes at least
+    assert [f(b"crc64", n) for n in (1024, 4096, 16384, 65536, 262144)] == [4, 4, 8, 32, 64]
     assert f(b"crc64", 1 << 20) == 64
     assert f(b"crc32c", 64) == 1
     assert f(b"crc16", 4096) == -1  # crc16 has no GPU kernel (CPU header path only)

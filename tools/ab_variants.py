@@ -27,6 +27,9 @@ SHAPES = {
     "f2k": ("crc32c", 131072, 2048, 0x4D43310000000002),
     "f8k": ("crc32c", 65536, 8192, 0x4D43310000000002),
     "f16k": ("crc32c", 65536, 16384, 0x4D43310000000002),
+    "g4k": ("crc64", 65536, 4096, 0x4D43310000000003),
+    "g16k": ("crc64", 32768, 16384, 0x4D43310000000003),
+    "g64k": ("crc64", 16384, 65536, 0x4D43310000000003),
     "c3": ("crc64", 8192, 1 << 20, 0x4D43310000000003),
     "c4": ("crc32c", 262144, None, 0x4D43310000000004),   # offsets table, U[64 B, 64 KiB]
     "c4_64": ("crc64", 262144, None, 0x4D43310000000004),
