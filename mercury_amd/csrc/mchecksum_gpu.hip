@@ -305,6 +305,12 @@ struct KLaunch {
     int block, blocks_per_cu;
 };
 
+// MCHECKSUM_GPU_LOG2G=g: 2^g lanes per payload for every fixed batch (A/B)
+bool lg_forced() {
+    const char *env = getenv("MCHECKSUM_GPU_LOG2G");
+    return env && env[0];
+}
+
 int choose_log2g(size_t len, int width) {
     const char *env = getenv("MCHECKSUM_GPU_LOG2G");
     if (env && env[0]) {
@@ -416,6 +422,14 @@ unsigned grid_for(const DevCtx *c, uint64_t waves_needed, const KLaunch &kl) {
     uint64_t blocks = (waves_needed + wpb - 1) / wpb;
     if (blocks > (uint64_t)c->cus * kl.blocks_per_cu) blocks = (uint64_t)c->cus * kl.blocks_per_cu;
     return blocks ? (unsigned)blocks : 1u;
+}
+
+// The table pack for another lanes-per-payload choice (cached per device).
+int repack(DevCtx *c, const char *method, int log2g, const void **pack) {
+    int width = 0;
+    const int idx = gpu_model(method, &width);
+    std::lock_guard<std::mutex> lk(g_mu);
+    return get_pack(c, idx, log2g, pack);
 }
 
 int prologue(const char *method, int log2g, int *width, DevCtx **c, const void **pack) {
@@ -650,21 +664,33 @@ int mchecksum_gpu_checksum_fixed(const char *hash_method, const void *dev_base, 
     if (!mchecksum_gpu_available()) return set_err(MCHECKSUM_GPU_ENODEV, "no HIP device");
     int width = 0;
     if (gpu_model(hash_method, &width) >= 0 && width == 32 && use_light((uint64_t)len * count, true)) {
-        const int lg = light_log2g(len);
+        int lg = light_log2g(len);
         DevCtx *c = nullptr;
         const void *pack = nullptr;
         int rc = prologue(hash_method, lg, &width, &c, &pack);
         if (rc) return rc;
         if (count == 0) return MCHECKSUM_GPU_OK;
+        // light layout: no more lanes per payload than give every CU about
+        // four waves (4096 x 4 KiB: 16 lanes -12% against 64; 1024 x 4 KiB
+        // keeps 64, profiles/r04/ab_small_knobs.log)
+        if (!lg_forced())
+            while (lg > 0 && ((uint64_t)count << (lg - 1)) >= (uint64_t)c->cus * 4 * 64) lg--;
+        if ((rc = repack(c, hash_method, lg, &pack))) return rc;
         return launch_fixed(c, gpu_model(hash_method, &width), pack, width, lg, dev_base, stride, len, count, dev_out,
                             stream, true);
     }
-    const int lg = choose_log2g(len, width);
+    int lg = choose_log2g(len, width);
     DevCtx *c = nullptr;
     const void *pack = nullptr;
     int rc = prologue(hash_method, lg, &width, &c, &pack);
     if (rc) return rc;
     if (count == 0) return MCHECKSUM_GPU_OK;
+    // a batch too small for the chosen payloads per wave to occupy every wave
+    // slot (16 per CU) gets more lanes per payload: 8192 x 4 KiB at 4 lanes
+    // ran 2x slower than at 64 (profiles/r04/ab_small_knobs.log)
+    if (!lg_forced())
+        while (lg < CRC_GPU_MAX_LOG2G && ((count + (64u >> lg) - 1) >> (6 - lg)) < (uint64_t)c->cus * 16) lg++;
+    if ((rc = repack(c, hash_method, lg, &pack))) return rc;
     return launch_fixed(c, gpu_model(hash_method, &width), pack, width, lg, dev_base, stride, len, count, dev_out,
                         stream, false);
 }

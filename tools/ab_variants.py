@@ -27,6 +27,7 @@ SHAPES = {
     "f2k": ("crc32c", 131072, 2048, 0x4D43310000000002),
     "f8k": ("crc32c", 65536, 8192, 0x4D43310000000002),
     "f16k": ("crc32c", 65536, 16384, 0x4D43310000000002),
+    "s8192": ("crc32c", 8192, 4096, 0x4D43310000000002),     # 32 MiB: just past the light layout
     "g4k": ("crc64", 65536, 4096, 0x4D43310000000003),
     "g16k": ("crc64", 32768, 16384, 0x4D43310000000003),
     "g64k": ("crc64", 16384, 65536, 0x4D43310000000003),
