@@ -28,6 +28,7 @@ SHAPES = {
     "f8k": ("crc32c", 65536, 8192, 0x4D43310000000002),
     "f16k": ("crc32c", 65536, 16384, 0x4D43310000000002),
     "s8192": ("crc32c", 8192, 4096, 0x4D43310000000002),     # 32 MiB: just past the light layout
+    "s2048": ("crc32c", 2048, 4096, 0x4D43310000000002),
     "g4k": ("crc64", 65536, 4096, 0x4D43310000000003),
     "g16k": ("crc64", 32768, 16384, 0x4D43310000000003),
     "g64k": ("crc64", 16384, 65536, 0x4D43310000000003),
