@@ -210,7 +210,9 @@ mchecksum_gpu_checksum_xdr(const char *hash_method,
     uint8_t *dev_status, void *stream);
 
 /* Lanes cooperating on one payload that checksum_fixed would choose for
- * this length (1..64), for reporting; -1 on error. */
+ * this length (1..64) in a batch large enough to fill the device; a smaller
+ * batch gets more lanes per payload until it fills every wave slot (a small
+ * one in the light layout may get fewer).  For reporting; -1 on error. */
 MCHECKSUM_PUBLIC int
 mchecksum_gpu_lanes_per_payload(const char *hash_method, size_t len);
 
