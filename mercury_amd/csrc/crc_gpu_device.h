@@ -197,7 +197,11 @@ struct BatchArgs {
     uint32_t split_lds;
 };
 // Piece size of a split payload: 256 KiB = 256 steps of the G = 64 loop.
-constexpr uint64_t kSplitBytes = 256u << 10;
+// (A/B, round 4: 128 KiB pieces +2.9%, 512 KiB +6.8% on C3, profiles/r04/ab_split_piece.log)
+#ifndef MCK_SPLIT_KIB
+#define MCK_SPLIT_KIB 256
+#endif
+constexpr uint64_t kSplitBytes = (uint64_t)MCK_SPLIT_KIB << 10;
 // Payloads per queue chunk whose pieces a workgroup can combine in LDS.
 constexpr uint32_t kSplitAcc = 16;
 
