@@ -371,12 +371,13 @@ __device__ __forceinline__ void lds_st(T *p, T v) {
     __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// Every wait in the queue protocol is bounded: a wait that exceeds ~1 s (or a
-// wave that takes more slots than the launch has) counts a fault in
-// g_mck_queue_faults (read by mchecksum_gpu_queue_faults()) and
-// leaves the loop, so a protocol failure shows up as a fault count and wrong
-// values in tests instead of a wedged GPU.  Diagnostic builds (-DMCK_TRACE=1)
-// also record where (g_mck_qdiag).
+// Every wait in the queue protocol is bounded in time: a wait still unmet
+// after kWaitTicks of the constant 100 MHz real-time counter (1 s; or a wave
+// that takes more slots than the launch has) counts a fault in
+// g_mck_queue_faults (read by mchecksum_gpu_queue_faults()) and leaves the
+// loop, so a protocol failure shows up as a fault count and a failed call
+// instead of a wedged GPU.  Diagnostic builds (-DMCK_TRACE=1) also record
+// where (g_mck_qdiag).
 __device__ unsigned int g_mck_queue_faults;
 #if MCK_TRACE
 __device__ unsigned long long g_mck_qdiag[4 * 64];
@@ -402,12 +403,46 @@ __device__ __noinline__ void queue_fault(uint32_t kind, uint64_t a, uint64_t b) 
     (void)b;
 #endif
 }
-constexpr uint32_t kSpinMax = 1u << 24;
-#define MCK_SPIN_GUARD(cnt, kind, A_, B_) \
-    if (++(cnt) > kSpinMax) {             \
-        queue_fault(kind, A_, B_);        \
-        break;                            \
+// A wait's deadline, on wall_clock64() -- the 100 MHz real-time counter,
+// independent of the shader clock and of how slow each poll gets under
+// contention (round 4's reverted in-kernel zeroing hung with 8192 waves
+// polling one line: an iteration count had bounded nothing).  The counter is
+// read on every 16th poll only (the polls stay tight: the ring-entry wait sits
+// on the path of every unit taken) and the first read starts the clock.
+// Round 4 and before counted polls (2^24 / 2^22) instead.
+#ifndef MCK_WAIT_TICKS
+#define MCK_WAIT_TICKS 100000000ull  // 1 s at 100 MHz
+#endif
+constexpr uint64_t kWaitTicks = MCK_WAIT_TICKS;
+struct Deadline {
+    uint64_t t0 = 0;
+    uint32_t polls = 0;
+    // true once this wait has lasted kWaitTicks (call once per poll)
+    __device__ __forceinline__ bool passed() {
+        if ((++polls & 15u) != 1u) return false;
+        const uint64_t now = wall_clock64();
+        if (polls == 1u) {
+            t0 = now;
+            return false;
+        }
+        return now - t0 > kWaitTicks;
     }
+};
+#define MCK_WAIT_GUARD(dl, kind, A_, B_) \
+    if ((dl).passed()) {                 \
+        queue_fault(kind, A_, B_);       \
+        break;                           \
+    }
+
+#if MCK_QFAULT_TEST
+// Test builds: which failure the qfault library injects (set from
+// MCHECKSUM_GPU_QFAULT_MODE before every launch, gpu_host.h): 0 = a wave gives
+// up one unit without waiting (workgroup 3, the first unit of its second
+// chunk); 1 = "stall": workgroup 3 never publishes its third chunk, so its
+// waves wait out the deadline; in the segment scan, the faulting block never
+// publishes its look-back descriptor, so its successors wait out theirs.
+__device__ unsigned int g_mck_qfault_mode;
+#endif
 
 // Steal order (MCK_STEAL_ROT=0: every thief starts at home + 1).  On since
 // round 3: never slower in four one-process A/Bs over rounds 3-4 (headline
@@ -450,12 +485,11 @@ __device__ uint64_t wg_fetch(WgQueue *L, unsigned long long *q, uint64_t nch) {
 __device__ bool wg_publish(WgQueue *L, uint32_t seq, uint64_t id, uint32_t cl) {
     const uint32_t r = seq % kWgRing;
     bool ok = true;
-    uint32_t spins = 0;
-    (void)spins;
+    Deadline dl;
     if (seq >= kWgRing)
         while (lds_ld(&L->reads[r]) != (1u << cl)) {
             __builtin_amdgcn_s_sleep(1);
-            if (++spins > kSpinMax) {
+            if (dl.passed()) {
                 queue_fault(1, seq, lds_ld(&L->reads[r]));
                 ok = false;
                 break;
@@ -580,15 +614,14 @@ __device__ __forceinline__ bool for_each_unit(WgQueue *L, unsigned long long *qu
                 if (l0) {
                     t = atomicAdd(&L->slot, 1u);
                     const uint32_t seq = t >> cl, r = seq % kWgRing;
-                    uint32_t spins = 0;
-                    (void)spins;
+                    Deadline dl;
 #if MCK_TRACE
                     const unsigned long long w0 = wall_clock64();
                     unsigned long long f0 = 0;
 #endif
                     while (((e = lds_ld(&L->entry[r])) >> 32) != seq) {
                         __builtin_amdgcn_s_sleep(1);
-                        MCK_SPIN_GUARD(spins, 2, seq, e)
+                        MCK_WAIT_GUARD(dl, 2, seq, e)
                     }
 #if MCK_TRACE
                     qs_wait += wall_clock64() - w0;
@@ -605,20 +638,30 @@ __device__ __forceinline__ bool for_each_unit(WgQueue *L, unsigned long long *qu
 #if MCK_TRACE
                         f0 = wall_clock64();
 #endif
-                        const uint64_t nid = (e & 0xFFFFFFFFull) == kNoChunk ? kNoChunk : wg_fetch(L, queue, nch);
+#if MCK_QFAULT_TEST
+                        // injected stall: workgroup 3 neither fetches nor
+                        // publishes its third chunk (no chunk is lost: the
+                        // other workgroups take every unit), so each of its
+                        // waves waits out the deadline on that ring entry
+                        const bool stall = g_mck_qfault_mode == 1u && blockIdx.x == 3 && seq == 1;
+#else
+                        constexpr bool stall = false;
+#endif
+                        const uint64_t nid =
+                            (e & 0xFFFFFFFFull) == kNoChunk || stall ? kNoChunk : wg_fetch(L, queue, nch);
 #if MCK_TRACE
                         const unsigned long long df = wall_clock64() - f0;
                         qs_n++;
                         qs_sum += df;
                         qs_max = df > qs_max ? df : qs_max;
 #endif
-                        if (!wg_publish(L, seq + 1, nid, cl)) flt = 1;
+                        if (!stall && !wg_publish(L, seq + 1, nid, cl)) flt = 1;
                     }
 #if MCK_QFAULT_TEST
                     // injected give-up: workgroup 3 drops the first unit of its
                     // second chunk (after its reads/publish duties, so the rest
                     // of the launch runs on)
-                    if (blockIdx.x == 3 && seq == 1 && (t & (cu - 1)) == 0 && !flt) {
+                    if (g_mck_qfault_mode == 0u && blockIdx.x == 3 && seq == 1 && (t & (cu - 1)) == 0 && !flt) {
                         queue_fault(9, seq, t);
                         e = kNoChunk;
                         flt = 1;

@@ -9,6 +9,8 @@
 
 #include <atomic>
 #include <cstdint>
+#include <cstdlib>
+#include <cstring>
 #include <deque>
 #include <mutex>
 #include <vector>
@@ -78,10 +80,24 @@ template <class T>
 struct Param {
     using type = T;
 };
+#if MCK_QFAULT_TEST
+// Test builds: the injected failure of the next launch (g_mck_qfault_mode,
+// crc_gpu_device.h; each translation unit has its own copy) from
+// MCHECKSUM_GPU_QFAULT_MODE ("stall", else the give-up), in stream order.
+static inline void qfault_mode_to_device(hipStream_t s) {
+    const char *env = getenv("MCHECKSUM_GPU_QFAULT_MODE");
+    static unsigned int modes[2] = {0u, 1u};  // static: the async copy's source must outlive the call
+    const unsigned int *m = &modes[env && strcmp(env, "stall") == 0 ? 1 : 0];
+    (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_mck_qfault_mode), m, sizeof(*m), 0, hipMemcpyHostToDevice, s);
+}
+#endif
 template <class... P>
 hipError_t launch_kernel(void (*k)(P...), dim3 grid, dim3 block, hipStream_t s, hipEvent_t stop,
                          typename Param<P>::type... args) {
     void *argv[] = {static_cast<void *>(&args)...};
+#if MCK_QFAULT_TEST
+    qfault_mode_to_device(s);
+#endif
     if (stop) return hipExtLaunchKernel(reinterpret_cast<const void *>(k), grid, block, argv, 0, s, nullptr, stop, 0);
     return hipLaunchKernel(reinterpret_cast<const void *>(k), grid, block, argv, 0, s);
 }

@@ -177,7 +177,14 @@ __device__ __forceinline__ bool seg_lookback(uint64_t *desc, uint64_t b, uint64_
                                              uint64_t tr, uint32_t lane, uint64_t *ep, uint64_t *ec, uint64_t *er,
                                              uint64_t fault_block) {
     uint64_t *me = desc + kDescWords * b;
-    if (lane == 0) {
+#if MCK_QFAULT_TEST
+    // injected stall (MCHECKSUM_GPU_QFAULT_MODE=stall): this block never
+    // publishes, so every later block waits out its deadline
+    const bool mute = g_mck_qfault_mode == 1u && b == fault_block;
+#else
+    constexpr bool mute = false;
+#endif
+    if (lane == 0 && !mute) {
         st_relaxed(me + 1, tp);
         st_relaxed(me + 2, tc);
         st_relaxed(me + 3, tr);
@@ -192,10 +199,10 @@ __device__ __forceinline__ bool seg_lookback(uint64_t *desc, uint64_t b, uint64_
     bool ok = true;
     if (b > 0) {
         int64_t k = (int64_t)b - 1;  // window: blocks k, k - 1, ..., k - 63 (lane order)
-        uint32_t spins = 0;
+        Deadline dl;  // 1 s of real time (crc_gpu_device.h)
         for (;;) {
 #if MCK_QFAULT_TEST
-            if (b == fault_block) {  // injected give-up (test builds, MCHECKSUM_GPU_QFAULT_SCAN)
+            if (b == fault_block && g_mck_qfault_mode == 0u) {  // injected give-up (test builds, MCHECKSUM_GPU_QFAULT_SCAN)
                 if (lane == 0) queue_fault(11, b, 0);
                 ok = false;
                 break;
@@ -211,7 +218,7 @@ __device__ __forceinline__ bool seg_lookback(uint64_t *desc, uint64_t b, uint64_
             const unsigned long long below = S >= 64 ? ~0ull : ((1ull << S) - 1);
             if (none & below) {  // a nearer block has not published yet
                 __builtin_amdgcn_s_sleep(1);
-                if (++spins > (1u << 22)) {
+                if (dl.passed()) {
                     if (lane == 0) queue_fault(10, b, (uint64_t)k);
                     ok = false;
                     break;
@@ -232,7 +239,7 @@ __device__ __forceinline__ bool seg_lookback(uint64_t *desc, uint64_t b, uint64_
             if (S < 64) break;
             k -= 64;
         }
-        if (lane == 0) {
+        if (lane == 0 && !mute) {
             st_relaxed(me + 4, sp + tp);
             st_relaxed(me + 5, sc + tc);
             st_relaxed(me + 6, sr | tr);
@@ -935,7 +942,8 @@ extern "C" {
 constexpr uint64_t kMaxSegs = 1ull << 40;
 uint64_t seg_map_cap(uint64_t nseg) { return nseg < (1ull << 32) ? 4 * nseg + 65536 : 0; }
 // Test builds (MCK_QFAULT_TEST): MCHECKSUM_GPU_QFAULT_SCAN=b makes scan block
-// b give up its look-back (tests/test_gpu_fail_closed.py); ~0 = none.
+// b give up its look-back -- or, with MCHECKSUM_GPU_QFAULT_MODE=stall, never
+// publish its descriptor (tests/test_gpu_fail_closed.py); ~0 = none.
 uint64_t scan_fault_block() {
     const char *env = MCK_QFAULT_TEST ? getenv("MCHECKSUM_GPU_QFAULT_SCAN") : nullptr;
     return env && env[0] ? strtoull(env, nullptr, 10) : ~0ull;

@@ -17,6 +17,7 @@ oracle by the parity suites).
 """
 import ctypes
 import os
+import time
 
 import numpy as np
 import pytest
@@ -216,4 +217,109 @@ def test_segment_scan_lookback_fault(gpu, qlib, monkeypatch):
     assert rc == 0
     torch.cuda.synchronize()
     assert int(word.item()) >= 1, "a scan whose look-back gave up must bump the error word"
+    assert qlib.mchecksum_gpu_queue_faults() - faults0 >= 1
+
+
+# Deadline waits (crc_gpu_device.h, Deadline): 1 s of the 100 MHz real-time
+# counter.  A launch whose wait is never satisfied must return well within
+# ~2 s and report itself failed -- whatever the per-poll cost under contention.
+STALL_MAX_S = 3.0
+
+
+def _timed(fn):
+    import torch
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    fn()
+    torch.cuda.synchronize()
+    return time.perf_counter() - t0
+
+
+@pytest.mark.parametrize("method", ["crc32c", "crc64"])
+def test_ring_entry_never_published_times_out(gpu, qlib, batch, method, monkeypatch):
+    """MCHECKSUM_GPU_QFAULT_MODE=stall: workgroup 3 never publishes its third
+    chunk, so its waves wait on that ring entry until the deadline.  The other
+    workgroups take every unit (no chunk is lost), so every CRC is right -- and
+    the call still reports the failed wait on the error word, exactly once."""
+    import torch
+    data, offs = batch
+    n = offs.numel() - 1
+    want = gpu.checksum_offsets(method, data, offs)
+    out = ~want
+    word = torch.zeros(1, dtype=torch.int32, device="cuda")
+    faults0 = qlib.mchecksum_gpu_queue_faults()
+    assert qlib.mchecksum_gpu_prepare(method.encode()) == 0
+    monkeypatch.setenv("MCHECKSUM_GPU_QFAULT_MODE", "stall")
+    qlib.mchecksum_gpu_set_error_word(word.data_ptr())
+    try:
+        rc = []
+        dt = _timed(lambda: rc.append(qlib.mchecksum_gpu_checksum_offsets(
+            method.encode(), data.data_ptr(), offs.data_ptr(), n, out.data_ptr(),
+            torch.cuda.current_stream().cuda_stream)))
+    finally:
+        qlib.mchecksum_gpu_set_error_word(None)
+    assert rc == [0]
+    print(f"stalled launch returned after {dt:.3f} s")
+    assert 0.9 <= dt <= STALL_MAX_S, f"deadline wait took {dt:.3f} s"
+    assert int(word.item()) == 1, "a launch whose waves timed out must bump the error word once"
+    assert qlib.mchecksum_gpu_queue_faults() - faults0 >= 1
+    assert torch.equal(out, want), "no unit is lost by the stall: every CRC must be right"
+
+
+def test_verify_with_stalled_entry_never_reads_clean(gpu, qlib, batch, monkeypatch):
+    """A verify launch whose waves time out: the mismatch count covers the
+    batch and every status ends flagged or truly verified -- never a stale 0."""
+    import torch
+    data, offs = batch
+    n = offs.numel() - 1
+    truth = gpu.checksum_offsets("crc32c", data, offs)
+    expected = truth.clone()
+    bad = np.arange(3, n, 11)
+    expected[torch.from_numpy(bad).cuda()] ^= 0x4000
+    status = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    mism = torch.zeros(1, dtype=torch.int32, device="cuda")
+    monkeypatch.setenv("MCHECKSUM_GPU_QFAULT_MODE", "stall")
+    dt = _timed(lambda: qlib.mchecksum_gpu_verify_offsets(
+        b"crc32c", data.data_ptr(), offs.data_ptr(), n, expected.data_ptr(), status.data_ptr(), mism.data_ptr(),
+        torch.cuda.current_stream().cuda_stream))
+    assert dt <= STALL_MAX_S, f"deadline wait took {dt:.3f} s"
+    st = status.cpu().numpy()
+    assert int(mism.item()) >= n
+    assert np.all(st[bad] == 1), "a real mismatch read as verified"
+    ok = st == 0
+    assert np.array_equal(expected.cpu().numpy()[ok], truth.cpu().numpy()[ok])
+
+
+def test_scan_descriptor_never_published_times_out(gpu, qlib, monkeypatch):
+    """MCHECKSUM_GPU_QFAULT_SCAN=1 with MCHECKSUM_GPU_QFAULT_MODE=stall: scan
+    block 1 never publishes its look-back descriptor, so block 2 waits until
+    its deadline.  The call returns within the bound and the error word
+    reports it."""
+    import torch
+    nseg = 3000  # three scan blocks
+    data = torch.empty(nseg * 4096 + 64, dtype=torch.uint8, device="cuda")
+    gpu.fill_splitmix(data, 0x5CA2)
+    segs = [data[i * 4096:(i + 1) * 4096] for i in range(nseg)]
+    batch = gpu.SegmentBatch(segs, np.arange(0, nseg + 1, 3))
+    torch.cuda.synchronize()
+    word = torch.zeros(1, dtype=torch.int32, device="cuda")
+    n, base = batch.nseg, batch.meta.data_ptr()
+    out = torch.zeros(batch.nobj, dtype=torch.int64, device="cuda")
+    faults0 = qlib.mchecksum_gpu_queue_faults()
+    assert qlib.mchecksum_gpu_prepare(b"crc64") == 0
+    work = torch.empty((qlib.mchecksum_gpu_segments_work_size(n) + 7) // 8, dtype=torch.int64, device="cuda")
+    monkeypatch.setenv("MCHECKSUM_GPU_QFAULT_SCAN", "1")
+    monkeypatch.setenv("MCHECKSUM_GPU_QFAULT_MODE", "stall")
+    qlib.mchecksum_gpu_set_error_word(word.data_ptr())
+    try:
+        rc = []
+        dt = _timed(lambda: rc.append(qlib.mchecksum_gpu_checksum_segments(
+            b"crc64", base, base + 8 * n, n, base + 16 * n, batch.nobj, work.data_ptr(), work.numel() * 8,
+            out.data_ptr(), torch.cuda.current_stream().cuda_stream)))
+    finally:
+        qlib.mchecksum_gpu_set_error_word(None)
+    assert rc == [0]
+    print(f"stalled scan returned after {dt:.3f} s")
+    assert 0.9 <= dt <= STALL_MAX_S, f"deadline wait took {dt:.3f} s"
+    assert int(word.item()) >= 1, "a scan whose look-back timed out must bump the error word"
     assert qlib.mchecksum_gpu_queue_faults() - faults0 >= 1

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Average rocprofv3 --pmc counters per kernel over dispatches (skipping the
-first, cold one).  usage: pmc_summary.py DIR [DIR...]"""
-import csv, glob, sys
+first, cold one).  usage: pmc_summary.py DIR [DIR...]
+PMC_KERNELS (comma-separated substrings, default batch_kernel) picks the kernels."""
+import csv, glob, os, sys
 from collections import defaultdict
 vals = defaultdict(lambda: defaultdict(list))
 for d in sys.argv[1:]:
@@ -19,7 +20,7 @@ for d in sys.argv[1:]:
                 for n, v in c.items():
                     vals[k][n].append(v)
 for k, c in vals.items():
-    if "batch_kernel" not in k:
+    if not any(s in k for s in os.environ.get("PMC_KERNELS", "batch_kernel").split(",")):
         continue
     print(k[:90])
     for n in sorted(c):
