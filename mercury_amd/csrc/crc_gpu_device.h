@@ -438,9 +438,11 @@ struct Deadline {
 // Test builds: which failure the qfault library injects (set from
 // MCHECKSUM_GPU_QFAULT_MODE before every launch, gpu_host.h): 0 = a wave gives
 // up one unit without waiting (workgroup 3, the first unit of its second
-// chunk); 1 = "stall": workgroup 3 never publishes its third chunk, so its
-// waves wait out the deadline; in the segment scan, the faulting block never
-// publishes its look-back descriptor, so its successors wait out theirs.
+// chunk; in the segment scan, block MCHECKSUM_GPU_QFAULT_SCAN gives up its
+// look-back); 1 = "stall": workgroup 3 never publishes its third chunk, so its
+// waves wait out the deadline; 2 = "scanstall": segment-scan block
+// MCHECKSUM_GPU_QFAULT_SCAN never publishes its look-back descriptor, so its
+// successors wait out theirs (nothing else is injected).
 __device__ unsigned int g_mck_qfault_mode;
 #endif
 

@@ -83,11 +83,13 @@ struct Param {
 #if MCK_QFAULT_TEST
 // Test builds: the injected failure of the next launch (g_mck_qfault_mode,
 // crc_gpu_device.h; each translation unit has its own copy) from
-// MCHECKSUM_GPU_QFAULT_MODE ("stall", else the give-up), in stream order.
+// MCHECKSUM_GPU_QFAULT_MODE ("stall" = 1, "scanstall" = 2, else the give-up
+// = 0), in stream order.
 static inline void qfault_mode_to_device(hipStream_t s) {
     const char *env = getenv("MCHECKSUM_GPU_QFAULT_MODE");
-    static unsigned int modes[2] = {0u, 1u};  // static: the async copy's source must outlive the call
-    const unsigned int *m = &modes[env && strcmp(env, "stall") == 0 ? 1 : 0];
+    static unsigned int modes[3] = {0u, 1u, 2u};  // static: the async copy's source must outlive the call
+    const int k = !env ? 0 : strcmp(env, "stall") == 0 ? 1 : strcmp(env, "scanstall") == 0 ? 2 : 0;
+    const unsigned int *m = &modes[k];
     (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_mck_qfault_mode), m, sizeof(*m), 0, hipMemcpyHostToDevice, s);
 }
 #endif

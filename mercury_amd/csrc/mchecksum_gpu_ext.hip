@@ -178,9 +178,9 @@ __device__ __forceinline__ bool seg_lookback(uint64_t *desc, uint64_t b, uint64_
                                              uint64_t fault_block) {
     uint64_t *me = desc + kDescWords * b;
 #if MCK_QFAULT_TEST
-    // injected stall (MCHECKSUM_GPU_QFAULT_MODE=stall): this block never
+    // injected stall (MCHECKSUM_GPU_QFAULT_MODE=scanstall): this block never
     // publishes, so every later block waits out its deadline
-    const bool mute = g_mck_qfault_mode == 1u && b == fault_block;
+    const bool mute = g_mck_qfault_mode == 2u && b == fault_block;
 #else
     constexpr bool mute = false;
 #endif
@@ -942,8 +942,8 @@ extern "C" {
 constexpr uint64_t kMaxSegs = 1ull << 40;
 uint64_t seg_map_cap(uint64_t nseg) { return nseg < (1ull << 32) ? 4 * nseg + 65536 : 0; }
 // Test builds (MCK_QFAULT_TEST): MCHECKSUM_GPU_QFAULT_SCAN=b makes scan block
-// b give up its look-back -- or, with MCHECKSUM_GPU_QFAULT_MODE=stall, never
-// publish its descriptor (tests/test_gpu_fail_closed.py); ~0 = none.
+// b give up its look-back -- or, with MCHECKSUM_GPU_QFAULT_MODE=scanstall,
+// never publish its descriptor (tests/test_gpu_fail_closed.py); ~0 = none.
 uint64_t scan_fault_block() {
     const char *env = MCK_QFAULT_TEST ? getenv("MCHECKSUM_GPU_QFAULT_SCAN") : nullptr;
     return env && env[0] ? strtoull(env, nullptr, 10) : ~0ull;
