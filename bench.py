@@ -87,6 +87,8 @@ def parse():
     p.add_argument("--parity-samples", type=int, default=64)
     p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                    help="nccl = RCCL (default); gloo only to rehearse the multi-rank flow on one GPU")
+    p.add_argument("--no-c5-strong", action="store_true",
+                   help="skip the c5_strong sub-record of the default (headline) run")
     return p.parse_args()
 
 
@@ -136,8 +138,13 @@ def main():
     # world size, 1 included: `torchrun --nproc-per-node 1 bench.py` runs the
     # same RCCL calls as the 8-GPU run (init, all_gather, all_reduce).
     dist_on = env_world is not None
+    ndev = torch.cuda.device_count()  # (counting devices does not initialise the GPU)
     if dist_on:
-        torch.cuda.set_device(local % torch.cuda.device_count())
+        # one GPU per rank: a run with more ranks than GPUs is refused (round 4
+        # mapped ranks modulo the count); only the gloo rehearsal may share one
+        if args.backend == "nccl" and (local >= ndev or world > ndev):
+            sys.exit(f"bench.py: {world} ranks (LOCAL_RANK {local}) but {ndev} GPU(s) visible: one GPU per rank")
+        torch.cuda.set_device(local if args.backend == "nccl" else local % max(ndev, 1))
         # The communication libraries may print connection notices on file
         # descriptor 1 (gloo's "[Gloo] Rank 0 is connected to ..."), which
         # would corrupt the one-JSON-line stdout contract: point fd 1 at
@@ -155,9 +162,31 @@ def main():
             sys.stdout.flush()
             os.dup2(saved_fd, 1)
             os.close(saved_fd)
+        # the line reports the group's own size and rank, not the environment's
+        world, rank = dist.get_world_size(), dist.get_rank()
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
+    coll_dev = dev if args.backend == "nccl" else torch.device("cpu")
+    # every rank's PCI address, gathered into the line: N distinct GPUs took part
+    pci = [float(x) for x in pci_address(torch, dev)]
+    if dist_on:
+        pt = torch.tensor(pci, dtype=torch.float64, device=coll_dev)
+        allp = [torch.empty_like(pt) for _ in range(world)]
+        dist.all_gather(allp, pt)
+        pcis = [pci_string(p.tolist()) for p in allp]
+    else:
+        pcis = [pci_string(pci)]
+    if args.backend == "nccl" and len(set(pcis)) != world:
+        sys.exit(f"bench.py: ranks share a GPU ({pcis}): one GPU per rank")
+
+    c5_strong = None
+    if args.config == "metric" and not args.no_c5_strong:
+        # BASELINE configs[4] in the same run, whatever flags the driver
+        # passes: C5's fixed 2^20 x 64 KiB batch split over the ranks (strong
+        # scaling).  Measured first, so the headline's dispatches are the last
+        # of their kernel in a profile of this command.
+        c5_strong = run_c5_strong(args, torch, dist, dist_on, rank, world, dev, coll_dev)
 
     from mercury_amd import gpu as G
     from mercury_amd.shard import batch_shard
@@ -292,7 +321,6 @@ def main():
     wall = time.perf_counter() - t0
     kern_ms = ev_start.elapsed_time(ev_end) / args.steps
 
-    coll_dev = dev if args.backend == "nccl" else torch.device("cpu")
     t = torch.tensor([wall, kern_ms], dtype=torch.float64, device=coll_dev)
     per_rank = [t.clone() for _ in range(world)]
     if dist_on:
@@ -348,8 +376,14 @@ def main():
             global_count=global_count, count=count, plan=plan, payload_bytes=payload_bytes, alg_bytes=alg_bytes,
             gib_s=gib_s, wall_max=wall_max, kern_ms_max=kern_ms_max, achieved=achieved, per_rank=per_rank,
             world=world, got=got, offsets_host=offsets_host, verify_note=verify_note,
-            process_group=dist.get_backend() if dist_on else None,
+            process_group=dist.get_backend() if dist_on else None, pcis=pcis,
             lanes=G.lanes_per_payload(method, length or 65536) if layout == "fixed" else 64))
+        if c5_strong is not None:
+            if not args.no_cpu_baseline:
+                c5_strong["parity"] = c5_parity(c5_strong.pop("_got"), c5_strong.pop("_firsts"), args.parity_samples)
+            c5_strong.pop("_got", None)
+            c5_strong.pop("_firsts", None)
+            result["c5_strong"] = c5_strong
         print(json.dumps(result), flush=True)
     if dist_on:
         dist.barrier()
@@ -391,7 +425,8 @@ def report(args, r):
                    "lanes_per_payload": r.lanes, "parallelism": f"shard{r.world}"},
         "world_size": r.world,
         "process_group": getattr(r, "process_group", None),
-        "per_rank": [{"rank": i, "wall_ms_per_step": round(w / args.steps * 1e3, 4), "kernel_ms": round(k, 4)}
+        "per_rank": [dict({"rank": i, "wall_ms_per_step": round(w / args.steps * 1e3, 4), "kernel_ms": round(k, 4)},
+                          **({"pci": r.pcis[i]} if getattr(r, "pcis", None) else {}))
                      for i, (w, k) in enumerate(r.per_rank)],
         "roofline": {"bound": "hbm", "achieved": round(r.achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(r.achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
@@ -412,6 +447,100 @@ def report(args, r):
     if r.verify_note:
         result["verify"] = r.verify_note
     return result
+
+
+def pci_address(torch, dev):
+    """(domain, bus, device) of the rank's GPU (-1 where torch does not say)."""
+    p = torch.cuda.get_device_properties(dev)
+    return tuple(int(getattr(p, k, -1)) for k in ("pci_domain_id", "pci_bus_id", "pci_device_id"))
+
+
+def pci_string(v):
+    d, b, f = (int(x) for x in v)
+    return f"{d:04x}:{b:02x}:{f:02x}" if min(d, b, f) >= 0 else "unknown"
+
+
+C5 = "c5"
+
+
+def run_c5_strong(args, torch, dist, dist_on, rank, world, dev, coll_dev):
+    """The c5_strong sub-record of the default run: BASELINE configs[4] --
+    CRC-32C over 2^20 x 64 KiB payloads, ONE global batch split into
+    contiguous rank shares (2^20 / N per rank) -- timed the same way as the
+    headline (barrier + synchronize around K back-to-back launches, max over
+    ranks), its CRCs gathered over the process group for the oracle check."""
+    from mercury_amd import gpu as G
+    from mercury_amd.shard import batch_shard
+    method, gcount, length, seed, _ = CONFIGS[C5]
+    plan = batch_shard(rank, world, gcount, length)
+    data = torch.empty(plan.nbytes + 64, dtype=torch.uint8, device=dev)
+    G.fill_splitmix(data, seed, first_word=plan.first_word)
+    out = torch.empty(plan.count, dtype=G.out_dtype(method), device=dev)
+    G.prepare(method)
+    for _ in range(args.warmup):
+        G.checksum_fixed(method, data, length, count=plan.count, out=out)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if dist_on:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(args.steps):
+        G.checksum_fixed(method, data, length, count=plan.count, out=out)
+    ev1.record()
+    torch.cuda.synchronize()
+    if dist_on:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    kern_ms = ev0.elapsed_time(ev1) / args.steps
+    t = torch.tensor([wall, kern_ms], dtype=torch.float64, device=coll_dev)
+    per_rank = [t.clone() for _ in range(world)]
+    crcs = out
+    if dist_on:
+        dist.all_gather(per_rank, t)
+        crcs = gather_shares(dist, out, plan.counts, world, coll_dev)
+    per_rank = [[float(x[0]), float(x[1])] for x in per_rank]
+    got = G.as_unsigned(crcs) if rank == 0 else None
+    del data, out
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    wall_max = max(w for w, _ in per_rank)
+    kern_max = max(k for _, k in per_rank)
+    total = float(gcount) * length * args.steps
+    alg = plan.nbytes + 4 * plan.count  # rank 0's share: payload bytes + 4-byte CRCs
+    return {
+        "config": C5,
+        "metric": "GiB/s checksummed (device-resident), CRC32c, 1M x 64 KiB payloads split over the GPUs (C5)",
+        "workload": (f"c5: {method} over {gcount} x {length} B payloads, one global batch split over {world} "
+                     f"GPU{'s' if world > 1 else ''} ({plan.count} on rank 0)"),
+        "value": round(total / wall_max / 2**30, 2),
+        "unit": "GiB/s",
+        "scaling": "strong",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(wall_max / args.steps * 1e3, 4),
+        "kernel_ms": round(kern_max, 4),
+        "roofline_frac": round(alg / (kern_max * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+        "per_rank": [{"rank": i, "wall_ms_per_step": round(w / args.steps * 1e3, 4), "kernel_ms": round(k, 4)}
+                     for i, (w, k) in enumerate(per_rank)],
+        "_got": got,
+        "_firsts": share_firsts(plan, "fixed", world, plan.count),
+    }
+
+
+def c5_parity(got, firsts, samples):
+    """The c5_strong CRCs vs the oracle (rank 0, after timing): the first and
+    last payload of every rank's share and `samples` random payloads of the
+    global batch, regenerated from the splitmix stream on the host."""
+    from oracle import oracle as O
+    method, gcount, length, seed, _ = CONFIGS[C5]
+    rng = np.random.default_rng(0xC5)
+    idx = sorted(set(firsts) | set(int(i) for i in rng.integers(0, gcount, samples)))
+    bad = [i for i in idx if int(got[i]) != int(O.splitmix_batch_fixed(method, seed, length, length, i, 1)[0])]
+    if bad:
+        return f"MISMATCH {len(bad)}/{len(idx)} sampled payloads (first {bad[:4]}) vs oracle"
+    return f"bit-exact ({len(idx)} payloads: both ends of every share + {samples} random, vs oracle)"
 
 
 def bench_c1(args):

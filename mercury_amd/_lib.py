@@ -107,5 +107,11 @@ def load_bench_library(path: str = BENCH_LIB_PATH) -> ctypes.CDLL:
     B = ctypes.CDLL(path)
     B.mck_bench_fill_splitmix.argtypes = [c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, c_void_p]
     B.mck_bench_fill_splitmix.restype = c_int
+    B.mck_bench_host_alloc.argtypes = [ctypes.c_uint64]
+    B.mck_bench_host_alloc.restype = c_void_p
+    B.mck_bench_host_free.argtypes = [c_void_p]
+    B.mck_bench_host_free.restype = c_int
+    B.mck_bench_gate.argtypes = [c_void_p, c_void_p, ctypes.c_double, c_void_p]
+    B.mck_bench_gate.restype = c_int
     _bench = B
     return B

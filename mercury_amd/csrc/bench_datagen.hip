@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstring>
 
 namespace {
 
@@ -53,5 +54,48 @@ extern "C" __attribute__((visibility("default"))) int mck_bench_fill_splitmix(vo
                            first_word);
     }
     if (nbytes & 7) hipLaunchKernelGGL(tail_kernel, dim3(1), dim3(1), 0, s, (uint8_t *)dev, nbytes, seed, first_word);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// Test utility (tests/test_gpu_slots.py): hold a stream until the host
+// releases it.  One wave polls a word of host memory (mck_bench_host_alloc:
+// coherent, mapped into the device) until it reads non-zero, or until
+// max_ticks of the 100 MHz real-time counter have passed -- then *expired = 1
+// (the test fails rather than the stream staying blocked).  Unlike a sleep
+// kernel, the hold ends exactly when the test says so.
+namespace {
+__global__ __launch_bounds__(64) void gate_kernel(const uint32_t *flag, uint32_t *expired, uint64_t max_ticks) {
+    const uint64_t t0 = wall_clock64();
+    for (;;) {
+        if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) break;
+        if (wall_clock64() - t0 > max_ticks) {
+            if (threadIdx.x == 0) __hip_atomic_store(expired, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(32);
+    }
+}
+}  // namespace
+
+extern "C" __attribute__((visibility("default"))) void *mck_bench_host_alloc(uint64_t nbytes) {
+    void *p = nullptr;
+    if (hipHostMalloc(&p, nbytes, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) return nullptr;
+    memset(p, 0, nbytes);
+    return p;
+}
+
+extern "C" __attribute__((visibility("default"))) int mck_bench_host_free(void *p) {
+    return hipHostFree(p) == hipSuccess ? 0 : -1;
+}
+
+extern "C" __attribute__((visibility("default"))) int mck_bench_gate(const uint32_t *flag, uint32_t *expired,
+                                                                     double max_seconds, void *stream) {
+    if (!flag || !expired || !(max_seconds > 0) || max_seconds > 60) return -1;
+    void *df = nullptr, *de = nullptr;
+    if (hipHostGetDevicePointer(&df, const_cast<uint32_t *>(flag), 0) != hipSuccess ||
+        hipHostGetDevicePointer(&de, expired, 0) != hipSuccess)
+        return -1;
+    hipLaunchKernelGGL(gate_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, (const uint32_t *)df, (uint32_t *)de,
+                       (uint64_t)(max_seconds * 1e8));
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }

@@ -1992,10 +1992,15 @@ __global__ __launch_bounds__(kBlk64<MODE>, kWpe64<MODE>) void crc64_batch_kernel
         // (The host's check is repeated here: a mismatch is a fault, never a
         // silently wrong value.)
         const bool in_wg = a.split_lds && a.queue && split_chunks_whole(units, gridDim.x, pieces);
-        bool faulted = a.split_lds && !in_wg;
-        if (faulted && threadIdx.x == 0) queue_fault(13, units, pieces);
-        if (!faulted)
-            faulted = for_each_unit<true, false, true>(&wgq, a.queue, units, wave, nw, [&](uint64_t u, uint32_t r) {
+        if (a.split_lds && !in_wg) {  // host and device disagree: fail closed, reported once per launch
+            if (blockIdx.x == 0 && threadIdx.x < 64) {
+                if (threadIdx.x == 0) queue_fault(13, units, pieces);
+                fail_closed<false>(a);
+            }
+            return;
+        }
+        const bool faulted =
+            for_each_unit<true, false, true>(&wgq, a.queue, units, wave, nw, [&](uint64_t u, uint32_t r) {
                 const uint64_t p = u >> sl;
                 const uint32_t q = (uint32_t)u & (pieces - 1);
                 const uint64_t x = payload64_aligned<6, NT, S::ops_global>(

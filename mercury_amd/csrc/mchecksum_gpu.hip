@@ -225,16 +225,23 @@ SlotRef queue_slot(DevCtx *c, void *stream) {
     }
     if (c->idle.empty() && c->in_flight.empty())  // first use on this device: every slot idle, slot 0 on top
         for (uint32_t k = c->nslots; k-- > 0;) c->idle.push_back(k);
-    // Reap: return the oldest in-flight slots whose launches have completed.
+    // Reap: look at the oldest in-flight slots; those whose launches have
+    // completed return to the pool, busy ones go to the back of the FIFO
+    // (left at the head, a few long-blocked launches -- a stream
+    // waiting on an event -- were looked at by every call while completed
+    // slots behind them were never reaped, and every launch fell back to the
+    // static split once the idle stack ran out).
     const uint32_t limit = c->idle.empty() ? kReapMax : kReapSome;
-    uint32_t looked = 0, busy = 0;
-    for (auto it = c->in_flight.begin(); it != c->in_flight.end() && looked < limit; looked++) {
-        if (slot_idle(c->slot[*it])) {
-            c->idle.push_back(*it);
-            it = c->in_flight.erase(it);
+    const size_t nlook = c->in_flight.size() < limit ? c->in_flight.size() : limit;
+    uint32_t busy = 0;
+    for (size_t k = 0; k < nlook; k++) {
+        const uint32_t i = c->in_flight.front();
+        c->in_flight.pop_front();
+        if (slot_idle(c->slot[i])) {
+            c->idle.push_back(i);
             c->n_reaped++;
         } else {
-            ++it;
+            c->in_flight.push_back(i);
             busy++;
         }
     }
@@ -673,9 +680,10 @@ int mchecksum_gpu_checksum_fixed(const char *hash_method, const void *dev_base, 
         // light layout: no more lanes per payload than give every CU about
         // four waves (4096 x 4 KiB: 16 lanes -12% against 64; 1024 x 4 KiB
         // keeps 64, profiles/r04/ab_small_knobs.log)
+        const int lg0 = lg;
         if (!lg_forced())
             while (lg > 0 && ((uint64_t)count << (lg - 1)) >= (uint64_t)c->cus * 4 * 64) lg--;
-        if ((rc = repack(c, hash_method, lg, &pack))) return rc;
+        if (lg != lg0 && (rc = repack(c, hash_method, lg, &pack))) return rc;
         return launch_fixed(c, gpu_model(hash_method, &width), pack, width, lg, dev_base, stride, len, count, dev_out,
                             stream, true);
     }
@@ -688,9 +696,11 @@ int mchecksum_gpu_checksum_fixed(const char *hash_method, const void *dev_base, 
     // a batch too small for the chosen payloads per wave to occupy every wave
     // slot (16 per CU) gets more lanes per payload: 8192 x 4 KiB at 4 lanes
     // ran 2x slower than at 64 (profiles/r04/ab_small_knobs.log)
+    const int lg0 = lg;
     if (!lg_forced())
         while (lg < CRC_GPU_MAX_LOG2G && ((count + (64u >> lg) - 1) >> (6 - lg)) < (uint64_t)c->cus * 16) lg++;
-    if ((rc = repack(c, hash_method, lg, &pack))) return rc;
+    // (the pack for another width only: repack takes g_mu)
+    if (lg != lg0 && (rc = repack(c, hash_method, lg, &pack))) return rc;
     return launch_fixed(c, gpu_model(hash_method, &width), pack, width, lg, dev_base, stride, len, count, dev_out,
                         stream, false);
 }

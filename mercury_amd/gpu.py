@@ -228,6 +228,18 @@ def verify_messages(data: torch.Tensor, msg_offsets: torch.Tensor, payload_offse
     return status, mism
 
 
+def _torch_owned(stream, handle: int, device) -> bool:
+    """Whether `handle` (the hipStream_t a call ran on, given `stream` as passed)
+    is a stream torch created and never destroys: a torch.cuda.Stream from its
+    pool (not an ExternalStream wrapping a caller's handle) or the device's
+    default stream.  With stream=None the current stream may wrap an external
+    handle, which torch cannot tell apart here, so only the default stream
+    counts."""
+    if stream is None:
+        return handle == torch.cuda.default_stream(device).cuda_stream
+    return type(stream) is torch.cuda.Stream
+
+
 class SegmentBatch:
     """A scatter-gather batch prepared once: object j = the concatenation of
     segments[obj_first[j]:obj_first[j+1]] (default: one object), each segment a
@@ -280,12 +292,13 @@ class SegmentBatch:
             s = (torch.cuda.ExternalStream(h) if h else torch.cuda.default_stream(self.device)) if track else None
             if track and self._last is not None and self._last[0] != h:
                 # the workspace is still the previous call's: this stream waits
-                # for it.  On a torch stream (never destroyed: torch's streams
-                # come from its pool) the event is recorded now, at the switch,
-                # after everything queued so far -- not after every call (a
-                # marker packet between the kernels costs ~3 us); a raw handle
-                # may be destroyed by then, so its event was recorded right
-                # after the call.
+                # for it.  On a stream torch owns (its pool's or the default
+                # stream: never destroyed) the event is recorded now, at the
+                # switch, after everything queued so far -- not after every
+                # call (a marker packet between the kernels costs ~3 us); any
+                # other stream (a raw handle, a torch.cuda.ExternalStream, or
+                # a current stream that may be one) may be destroyed by then,
+                # so its event was recorded right after the call.
                 ev = self._last[2]
                 if ev is None:
                     ev = torch.cuda.Event()
@@ -296,7 +309,7 @@ class SegmentBatch:
                                                         out.data_ptr(), h)
             if rc == 0 and track:
                 ev = None
-                if stream is not None and not hasattr(stream, "cuda_stream"):  # a raw hipStream_t
+                if not _torch_owned(stream, h, self.device):
                     ev = torch.cuda.Event()
                     ev.record(s)
                 self._last = (h, s, ev)
@@ -388,6 +401,42 @@ def fill_splitmix(t: torch.Tensor, seed: int, first_word: int = 0, stream=None) 
     if rc != 0:
         raise GpuChecksumError(f"fill_splitmix failed rc={rc}")
     return t
+
+
+class HostGate:
+    """Test utility (libmchecksum_bench.so): a kernel that holds a stream until
+    the host calls release() -- one wave polling a word of coherent host
+    memory -- or until max_seconds pass, which `expired` then reports.  Used
+    to keep launches queued for exactly as long as a test needs."""
+
+    def __init__(self):
+        self._B = load_bench_library()
+        self._mem = self._B.mck_bench_host_alloc(8)
+        if not self._mem:
+            raise GpuChecksumError("hipHostMalloc failed")
+        self._flag = ctypes.c_uint32.from_address(self._mem)
+        self._exp = ctypes.c_uint32.from_address(self._mem + 4)
+
+    def hold(self, stream, max_seconds: float = 20.0) -> None:
+        self._flag.value = 0
+        self._exp.value = 0
+        h = _stream_handle(stream)
+        if self._B.mck_bench_gate(self._mem, self._mem + 4, float(max_seconds), h) != 0:
+            raise GpuChecksumError("gate launch failed")
+
+    def release(self) -> None:
+        self._flag.value = 1
+
+    @property
+    def expired(self) -> bool:
+        return bool(self._exp.value)
+
+    def close(self) -> None:
+        if self._mem:
+            self.release()
+            torch.cuda.synchronize()
+            self._B.mck_bench_host_free(self._mem)
+            self._mem = None
 
 
 def as_unsigned(x: torch.Tensor):

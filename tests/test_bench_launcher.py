@@ -55,6 +55,23 @@ def test_world_size_mismatch_is_refused():
     assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
 
 
+def test_more_ranks_than_gpus_is_refused():
+    """Verdict r4: one GPU per rank -- a torchrun world larger than the
+    visible device count exits non-zero before forming the group (round 4
+    mapped ranks modulo the count, so two ranks could share a GPU and the
+    line would still read as N GPUs).  This container sees no GPU at all."""
+    env = dict(os.environ, WORLD_SIZE="2", RANK="1", LOCAL_RANK="1", MASTER_ADDR="127.0.0.1", MASTER_PORT="1")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "one GPU per rank" in r.stderr, r.stderr[-2000:]
+
+
+def test_pci_strings():
+    import bench
+    assert bench.pci_string([0, 0x75, 0]) == "0000:75:00"
+    assert bench.pci_string([-1, 3, 0]) == "unknown"
+
+
 def test_launcher_starts_torchrun_before_touching_the_gpu(monkeypatch):
     """--gpus N without torchrun: bench.py starts N ranks itself (127.0.0.1
     rendezvous) and returns their exit code."""

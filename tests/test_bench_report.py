@@ -89,7 +89,7 @@ def _worker(name, corrupt, rank, world, port, q):
             global_count=gc if layout != "segments" else gc * world, count=count, plan=plan,
             payload_bytes=payload_bytes, alg_bytes=payload_bytes + 4 * count, gib_s=1.0, wall_max=0.003,
             kern_ms_max=1.0, achieved=1.0, per_rank=[[0.003, 1.0]] * world, world=world, got=got, offsets_host=off,
-            verify_note=None, lanes=64)
+            verify_note=None, lanes=64, pcis=[f"0000:{0x11 * (i + 1):02x}:00" for i in range(world)])
         q.put(bench.report(args, r))
     dist.barrier()
     dist.destroy_process_group()
@@ -123,6 +123,8 @@ def test_two_rank_line_has_baseline_oracle_parity_and_traffic(name):
     assert all(v and v > 0 for v in prod.values()), (bd, cb.get("product_note"))
     assert res["parity"].startswith("bit-exact (") and "across all 2 shares vs oracle" in res["parity"], res["parity"]
     assert res["n_gpus"] == 2 and res["world_size"] == 2 and len(res["per_rank"]) == 2
+    # every rank's PCI address is in the line (bench.py gathers them; distinct on RCCL runs)
+    assert [p["pci"] for p in res["per_rank"]] == ["0000:11:00", "0000:22:00"]
     roof = res["roofline"]
     assert roof["traffic"] is not None and "rank 0's share" in roof["traffic_source"], roof
     assert res["scaling"] == ("weak" if name in ("segments", "weak_fixed") else "strong")

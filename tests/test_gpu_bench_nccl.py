@@ -59,3 +59,15 @@ def test_one_rank_nccl_line(config):
     assert res["parity"].startswith("bit-exact (") and res["parity"].endswith("vs oracle)"), res["parity"]
     assert res["value"] > 0 and res["roofline"]["frac"] > 0
     assert res["scaling"] == ("strong" if config == "c5" else "weak")
+    # the group's own world size, and the GPU each rank ran on
+    assert [p["rank"] for p in res["per_rank"]] == [0] and res["per_rank"][0]["pci"] != "unknown", res["per_rank"]
+    if config == "metric":
+        # BASELINE configs[4] measured in the same run whatever the flags:
+        # C5's 2^20 x 64 KiB global batch split over the ranks
+        c5 = res["c5_strong"]
+        assert c5["config"] == "c5" and c5["scaling"] == "strong" and c5["n_gpus"] == 1, c5
+        assert "1048576 x 65536 B payloads" in c5["workload"] and "(1048576 on rank 0)" in c5["workload"], c5
+        assert c5["value"] > 0 and 0 < c5["roofline_frac"] < 1 and len(c5["per_rank"]) == 1
+        assert c5["parity"].startswith("bit-exact ("), c5["parity"]
+    else:
+        assert "c5_strong" not in res

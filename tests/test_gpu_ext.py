@@ -329,6 +329,53 @@ def test_segment_batch_raw_stream_destroyed_between_calls(gpu, buf, oracle_mod):
         assert gpu.as_unsigned(o).tolist() == want
 
 
+@pytest.mark.parametrize("how", ["external", "current"])
+def test_segment_batch_external_stream_destroyed_between_calls(gpu, buf, oracle_mod, how):
+    """As above, with the raw handle wrapped in torch.cuda.ExternalStream --
+    passed as `stream` ("external") or made the current stream with
+    torch.cuda.stream(...) and stream=None ("current"): torch does not own
+    such a stream, so the guard event is recorded right after each call, never
+    later on a handle the caller has destroyed."""
+    import ctypes
+    import os
+    import torch
+    L = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so"))
+    L.hipStreamCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
+    L.hipStreamDestroy.argtypes = [ctypes.c_void_p]
+    host = _host(buf)
+    rng = np.random.default_rng(406)
+    segs, first = _objects(rng, buf.numel() - 64, 60)
+    batch = gpu.SegmentBatch([buf[o:o + n] for o, n in segs], first)
+    want = _want(oracle_mod, "crc64", host, segs, first)
+    outs = []
+    torch.cuda.synchronize()
+    for rep in range(6):
+        h = ctypes.c_void_p()
+        assert L.hipStreamCreateWithFlags(ctypes.byref(h), 1) == 0
+        o = torch.zeros(len(first) - 1, dtype=torch.int64, device="cuda")
+        torch.cuda.synchronize()
+        ext = torch.cuda.ExternalStream(h.value)
+        if how == "external":
+            batch.checksum("crc64", out=o, stream=ext)
+        else:
+            with torch.cuda.stream(ext):
+                batch.checksum("crc64", out=o)
+        assert batch._last[2] is not None, "no guard event recorded after a call on a stream torch does not own"
+        del ext
+        assert L.hipStreamDestroy(h.value) == 0  # with the call possibly still in flight
+        outs.append(o)
+    torch.cuda.synchronize()
+    for o in outs:
+        assert gpu.as_unsigned(o).tolist() == want
+    # a pool stream still defers its event to the switch (no per-call marker)
+    s1 = torch.cuda.Stream()
+    o = torch.zeros(len(first) - 1, dtype=torch.int64, device="cuda")
+    batch.checksum("crc64", out=o, stream=s1)
+    assert batch._last[2] is None
+    torch.cuda.synchronize()
+    assert gpu.as_unsigned(o).tolist() == want
+
+
 def test_segment_batch_calls_on_two_streams(gpu, buf, oracle_mod):
     """One SegmentBatch used on two streams back to back: the calls share its
     workspace, so the second waits for the first (gpu.SegmentBatch) and both

@@ -161,89 +161,123 @@ data = torch.from_numpy(np.concatenate([host, np.zeros(64, np.uint8)])).cuda()
 offs = torch.from_numpy(off).cuda()
 want = torch.from_numpy(O.batch_offsets("crc32c", host, off.astype(np.uint64)).astype(np.uint32).view(np.int32)).cuda()
 n = 2000
-# torch's sleep kernel: cycles per second of its clock
-a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-a.record(); torch.cuda._sleep(50_000_000); b.record(); torch.cuda.synchronize()
-per_s = 50_000_000 / max(a.elapsed_time(b) * 1e-3, 1e-6)
-A, B = torch.cuda.Stream(), torch.cuda.Stream()
-G.checksum_offsets("crc32c", data, offs, stream=B); torch.cuda.synchronize()  # warm-up
+gate = G.HostGate()
+A = torch.cuda.Stream()
+G.checksum_offsets("crc32c", data, offs, stream=A); torch.cuda.synchronize()  # warm-up
+
+
+def done_within(ev, seconds):
+    t0 = time.monotonic()
+    while not ev.query() and time.monotonic() - t0 < seconds:
+        time.sleep(0.0005)
+    return ev.query()
+
+
+# B: a stream on another hardware queue than A (GPU_MAX_HW_QUEUES = 4 queues
+# are shared round-robin by the process's streams): with A held by the gate,
+# a candidate whose small kernel completes does not sit behind A.
+gate.hold(A)
+B, tried = None, 0
+for prio in (0, -1):
+    for _ in range(8):
+        cand = torch.cuda.Stream(priority=prio)
+        tried += 1
+        with torch.cuda.stream(cand):
+            x = torch.ones(4, device="cuda") * 2
+            ev = torch.cuda.Event(); ev.record(cand)
+        if done_within(ev, 0.5):
+            B = cand
+            break
+    if B is not None:
+        break
+gate.release(); torch.cuda.synchronize()
+assert not gate.expired
+assert B is not None, f"no stream of {tried} runs beside a held stream"
+print("B found after", tried, "candidates")
+
+# 1) A held by the gate, then NSLOTS + 3 queue launches behind it: the first
+#    NSLOTS take every slot; the last 3 find none idle (all in flight, busy)
+#    and take the static split
 st0 = G.queue_stats()
-# 1) A: a ~3 s sleep, then NSLOTS + 3 queue launches behind it: the first
-#    NSLOTS take every slot; the last 3 find none idle (all in flight) and
-#    take the static split
 outs = torch.zeros((NSLOTS + 3, n), dtype=torch.int32, device="cuda")
 torch.cuda.synchronize()
+gate.hold(A)
 with torch.cuda.stream(A):
-    torch.cuda._sleep(int(3 * per_s))
     for k in range(NSLOTS + 3):
         G.checksum_offsets("crc32c", data, offs, out=outs[k], stream=A)
     ev_a = torch.cuda.Event(); ev_a.record(A)
 st1 = G.queue_stats()
-assert not ev_a.query(), "the sleep ended before the launches were queued"
+held = not ev_a.query()
+gate.release(); torch.cuda.synchronize()
+assert held and not gate.expired
 assert st1["slot"] - st0["slot"] == NSLOTS and st1["noslot"] - st0["noslot"] == 3, (st0, st1)
 assert st1["in_flight"] == NSLOTS and st1["busy_skip"] > st0["busy_skip"], (st0, st1)
-torch.cuda.synchronize()
 assert bool((outs == want).all()), torch.nonzero((outs != want).any(dim=1)).tolist()
+
 # 2) once they have completed, the pool is reaped: a launch gets a slot again
 st2 = G.queue_stats()
 o = G.checksum_offsets("crc32c", data, offs, stream=B); torch.cuda.synchronize()
 st3 = G.queue_stats()
 assert st3["slot"] - st2["slot"] == 1 and st3["reaped"] > st2["reaped"], (st2, st3)
 assert torch.equal(o, want)
-# 3) a busy slot is passed over: A holds ONE slot behind a ~3 s sleep (the
-#    oldest in flight); B then launches more than the pool holds, one at a
-#    time, each completed before the next: the reaper keeps finding B's
-#    completed slots behind A's busy one, and never hands A's out
-st4 = G.queue_stats()
-xa = torch.zeros(n, dtype=torch.int32, device="cuda")
-outs = torch.zeros((3 * NSLOTS, n), dtype=torch.int32, device="cuda")
-torch.cuda.synchronize()
-with torch.cuda.stream(A):
-    torch.cuda._sleep(int(3 * per_s))
-    G.checksum_offsets("crc32c", data, offs, out=xa, stream=A)
-    ev_a = torch.cuda.Event(); ev_a.record(A)
-blocked = 0
-for k in range(3 * NSLOTS):
-    G.checksum_offsets("crc32c", data, offs, out=outs[k], stream=B)
-    ev_b = torch.cuda.Event(); ev_b.record(B)
-    t0 = time.monotonic()
-    while not ev_b.query() and time.monotonic() - t0 < 5:
-        time.sleep(0.0005)
-    blocked += not ev_b.query()
-st5 = G.queue_stats()
-busy_now = not ev_a.query()
-torch.cuda.synchronize()
-print("pool ok", NSLOTS, st0, st1, st3, st4, st5, "A still busy:", busy_now, "B blocked:", blocked)
-assert bool((outs == want).all()) and torch.equal(xa, want)
-if busy_now and not blocked:  # B ran beside A's sleep: A's slot stayed busy throughout
-    assert st5["slot"] - st4["slot"] == 3 * NSLOTS + 1 and st5["noslot"] == st4["noslot"], (st4, st5)
-    assert st5["busy_skip"] - st4["busy_skip"] >= 2 * NSLOTS, (st4, st5)  # A's slot looked at and passed over
-    print("busy slot passed over")
-else:
-    print("inconclusive: B shares A's hardware queue or the sleep ended")
+
+
+def blocked_oldest(nheld, nb):
+    # nheld launches held behind the gate on A (the oldest slots in flight),
+    # then nb launches on B one at a time, each completed before the next:
+    # every B launch must get a slot -- the reaper passes the held ones over
+    # and finds B's completed slots behind them
+    s0 = G.queue_stats()
+    xa = torch.zeros((nheld, n), dtype=torch.int32, device="cuda")
+    ob = torch.zeros((nb, n), dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    gate.hold(A)
+    with torch.cuda.stream(A):
+        for k in range(nheld):
+            G.checksum_offsets("crc32c", data, offs, out=xa[k], stream=A)
+        ev_a = torch.cuda.Event(); ev_a.record(A)
+    for k in range(nb):
+        G.checksum_offsets("crc32c", data, offs, out=ob[k], stream=B)
+        ev_b = torch.cuda.Event(); ev_b.record(B)
+        assert done_within(ev_b, 5), f"B launch {k} did not complete beside the held stream"
+    s1 = G.queue_stats()
+    still = not ev_a.query()
+    gate.release(); torch.cuda.synchronize()
+    assert still and not gate.expired, "A was released before B finished"
+    assert bool((ob == want).all()) and bool((xa == want).all())
+    assert s1["slot"] - s0["slot"] == nheld + nb and s1["noslot"] == s0["noslot"], (nheld, s0, s1)
+    assert s1["busy_skip"] - s0["busy_skip"] >= nb, (nheld, s0, s1)  # held slots looked at and passed over
+    return s0, s1
+
+
+# 3) one busy slot passed over while B cycles through the pool 3 times
+print("one held", blocked_oldest(1, 3 * NSLOTS))
+# 4) ADVICE r4: as many held launches as one reap looks at (8) at the head of
+#    the FIFO: busy slots rotate to its back, so B's completed ones are still
+#    reaped once the idle stack runs out (before: every later launch took the
+#    static split until A was released)
+if NSLOTS >= 16:
+    print("eight held", blocked_oldest(8, 3 * NSLOTS))
+gate.close()
 assert G.queue_faults() == 0
+print("pool ok", NSLOTS)
 """
 
 
-def _pool_run():
+def test_pool_hands_no_busy_slot_out():
+    """A fresh process with a 16-slot pool (MCHECKSUM_GPU_QUEUE_SLOTS=16),
+    streams held by a host-released gate kernel (not a timed sleep), and a
+    second stream probed to run beside the held one: launches queued behind
+    the gate take every slot and the rest take the static split; the pool
+    refills once they complete; a slot whose launch is held is passed over
+    while other launches cycle through the pool -- also with eight held
+    launches at the head of the in-flight FIFO.  Every result is exact.
+    One process, one conclusive outcome (round 4 retried in a second process
+    when the two streams shared a hardware queue)."""
     r = subprocess.run([sys.executable, "-c", POOL, ROOT], capture_output=True, text=True, timeout=200,
-                       env=dict(os.environ, MCHECKSUM_GPU_QUEUE_SLOTS="8", MCHECKSUM_GPU_LIGHT="0"))
+                       env=dict(os.environ, MCHECKSUM_GPU_QUEUE_SLOTS="16", MCHECKSUM_GPU_LIGHT="0"))
     print(r.stdout[-3000:])
     assert r.returncode == 0 and "pool ok" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
-    return r.stdout
-
-
-def test_pool_hands_no_busy_slot_out():
-    """A fresh process with an 8-slot pool (MCHECKSUM_GPU_QUEUE_SLOTS=8):
-    launches queued behind a sleep take every slot and the rest take the
-    static split; the pool refills once they complete; and a slot whose launch
-    is still queued is passed over while other launches cycle through the
-    pool.  Every result is exact."""
-    out = _pool_run()
-    if "busy slot passed over" not in out:
-        # B's stream shared A's hardware queue (GPU_MAX_HW_QUEUES = 4): once
-        # more with a fresh pair of streams in a new process
-        assert "busy slot passed over" in _pool_run()
 
 
 def test_sticky_error_before_a_queue_launch(gpu, hip, small_batch):
