@@ -20,6 +20,11 @@ GOBJS     := $(BUILD)/mchecksum_gpu.o $(BUILD)/mchecksum_gpu_ext.o
 
 QFAULTLIB := $(BUILD)/libmchecksum_qfault.so
 
+# Source digest compiled into the libraries (tools/src_digest.py): a test
+# compares it with the tree, so the tested binary is provably HEAD's sources.
+STAMP_SRCS := $(sort $(wildcard $(CSRC)/*.c $(CSRC)/*.h $(CSRC)/*.hip include/*.h))
+STAMP     := $(BUILD)/src_stamp.o
+
 all: $(LIB) $(BENCHLIB) oracle $(BUILD)/c1_bench $(QFAULTLIB) $(BUILD)/libcpu_batch.so
 
 $(BUILD) $(LIBDIR):
@@ -37,7 +42,13 @@ $(BUILD)/mchecksum_gpu_ext.o: $(CSRC)/mchecksum_gpu_ext.hip $(wildcard $(CSRC)/*
 $(BUILD)/bench_datagen.o: $(CSRC)/bench_datagen.hip | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) $(INC) -c $< -o $@
 
-$(LIB): $(COBJS) $(GOBJS) | $(LIBDIR)
+$(BUILD)/src_stamp.c: $(STAMP_SRCS) tools/src_digest.py | $(BUILD)
+	python3 tools/src_digest.py --c-source $@ $(STAMP_SRCS)
+
+$(STAMP): $(BUILD)/src_stamp.c
+	$(CC) $(CFLAGS) -c $< -o $@
+
+$(LIB): $(COBJS) $(GOBJS) $(STAMP) | $(LIBDIR)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^ -lpthread -Wl,-soname,libmchecksum.so.2
 	ln -sf libmchecksum.so $(LIBDIR)/libmchecksum.so.2
 
@@ -50,10 +61,10 @@ $(BUILD)/qfault_gpu.o: $(CSRC)/mchecksum_gpu.hip $(wildcard $(CSRC)/*.h) include
 $(BUILD)/qfault_gpu_ext.o: $(CSRC)/mchecksum_gpu_ext.hip $(wildcard $(CSRC)/*.h) include/mchecksum_gpu.h | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -DMCK_QFAULT_TEST=1 $(INC) -c $< -o $@
 
-$(QFAULTLIB): $(COBJS) $(BUILD)/qfault_gpu.o $(BUILD)/qfault_gpu_ext.o
+$(QFAULTLIB): $(COBJS) $(BUILD)/qfault_gpu.o $(BUILD)/qfault_gpu_ext.o $(STAMP)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^ -lpthread
 
-$(BENCHLIB): $(BUILD)/bench_datagen.o | $(LIBDIR)
+$(BENCHLIB): $(BUILD)/bench_datagen.o $(STAMP) | $(LIBDIR)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^
 
 oracle:

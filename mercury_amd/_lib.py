@@ -98,6 +98,34 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     return L
 
 
+# The sources libmchecksum is built from (the Makefile's STAMP_SRCS): their
+# digest is compiled into each library (tools/src_digest.py), so a loaded
+# library can be checked against the tree beside it.
+_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def tree_source_digest() -> str:
+    """sha256 over (path, NUL, bytes, NUL) of mercury_amd/csrc/*.{c,h,hip} and
+    include/*.h in path order -- tools/src_digest.py's algorithm."""
+    import glob
+    import hashlib
+    paths = []
+    for pat in ("mercury_amd/csrc/*.c", "mercury_amd/csrc/*.h", "mercury_amd/csrc/*.hip", "include/*.h"):
+        paths += glob.glob(os.path.join(_ROOT, pat))
+    h = hashlib.sha256()
+    for rel in sorted(os.path.relpath(p, _ROOT) for p in paths):
+        h.update(rel.encode() + b"\0")
+        with open(os.path.join(_ROOT, rel), "rb") as f:
+            h.update(f.read())
+        h.update(b"\0")
+    return h.hexdigest()
+
+
+def library_source_digest(lib: ctypes.CDLL) -> str:
+    """The source digest compiled into a loaded libmchecksum build."""
+    return (ctypes.c_char * 65).in_dll(lib, "mchecksum_build_source_digest").value.decode()
+
+
 def load_bench_library(path: str = BENCH_LIB_PATH) -> ctypes.CDLL:
     global _bench
     if _bench is not None:

@@ -85,6 +85,30 @@ constexpr uint32_t kL64Hi = 32768;
 constexpr uint32_t kL64Main = kL64Hi + 4 * 256;
 #endif
 constexpr uint32_t kL64Bytes = kL64Main + CRC64_NOPS_MAX * 2048;
+// The 11-lookup fold (kFold11, round 5) for the one-workgroup-per-CU kernels
+// (aligned fixed batches: C3; the merged segment pass).  The 12-lookup fold
+// keeps C3's LDS array ~82% busy (SQ_LDS_IDX_ACTIVE over the launch's cycles,
+// profiles/r05/sq_c3.txt): CRC-64 is LDS-bound, at 2 array cycles per
+// ds_read_b64 and 12 per 8-byte word.  With a whole CU's LDS, bits 0..6 of
+// bytes 6 and 7 and two 7-bit gathers of the low bits go to 7-bit tables
+// replicated 32x (32 KiB each): f5 over bytes 0..5 (6 lookups), 4 x f7, one
+// 6-bit pair table -- 11 lookups per word, 29 VALU instead of 26.  Map:
+//   [512, 2048)        f5[0..5] (256 B each, unreplicated)
+//   [2048, 67584)      f7[0], f7[1] (entry v at v*256 + lane copy*8)
+//   [67584, 79872)     butterfly operators Z^-(16*2^k), k < 6 (kL64Main, as
+//                      in the mixed operator mode)
+//   [79872, 145408)    f7[2], f7[3]
+//   [145408, 161792)   f6b (x32)
+// An address is the lane-copy register (byte 0: copy offset, byte 1: the
+// index, byte 2: the 64 KiB region) plus the DS immediate offset (< 64 KiB).
+enum Fold : int { kFold12 = 0, kFold11 = 1 };
+constexpr uint32_t kF11F5 = 512;
+constexpr uint32_t kF11F7a = 2048;
+constexpr uint32_t kF11F7c = kL64Main + 6 * 2048;
+constexpr uint32_t kF11F6 = kF11F7c + 2 * 32768;
+constexpr uint32_t kF11Bytes = kF11F6 + 16384;
+static_assert(kF11F7a + 2 * 32768 == kL64Main, "butterflies follow f7[0..1]");
+static_assert(kF11F7c == 65536 + 14336 && kF11F6 == 131072 + 14336, "region offsets in the lane registers");
 // CRC-64 is LDS/VALU-bound (table reads and their XOR tree); two 1024-thread
 // workgroups per CU (8 waves/SIMD) hide the LDS latency.  MCK_CRC64_SPLIT=1
 // (implied by MCK_CRC64_P6) reads the combine operators (touched once per
@@ -147,17 +171,35 @@ enum OpsMode : int { kOpsLds = 0, kOpsGlobal = 1, kOpsMix = 2 };
 #ifndef MCK_CRC64_ONE_WG_OPS_LDS
 #define MCK_CRC64_ONE_WG_OPS_LDS 1
 #endif
+// MCK_CRC64_FOLD11=1 builds the aligned one-workgroup-per-CU CRC-64 kernels
+// with the 11-lookup fold (butterflies in LDS, Z^-8 from global memory).  Off:
+// bit-exact (GPU parity suite green with it) but C3 -4.9% in one process
+// (1.3490 vs 1.2865 ms median, g64k -1.9%, g16k/g4k +-0.5%;
+// profiles/r05/ab_fold11.log).  Its counters (profiles/r05/sq_c3_fold11.txt)
+// show why: LDS-array cycles -8.2% (SQ_LDS_IDX_ACTIVE) and LDS issue waits
+// -37%, but VALU instructions +10.9% and shader cycles +6.2% -- the fold is
+// bound by VALU issue (26 VALU per 8-byte word at ~4 cycles each per SIMD:
+// ~90% of the launch's cycles), not by the LDS array, so a lookup traded for
+// three gather ops loses.
+#ifndef MCK_CRC64_FOLD11
+#define MCK_CRC64_FOLD11 0
+#endif
 template <int W, int MODE, bool LIGHT = false>
 struct Shape {
-    static constexpr bool ops_global = W == 64 && MODE == 0 && (MCK_CRC64_SPLIT || MCK_CRC64_P6) &&
-                                       !(MCK_CRC64_ONE_WG && MCK_CRC64_ONE_WG_OPS_LDS);  // 0 = kFixedAligned
     static constexpr bool two = W == 64 && ((MODE == 0 && !MCK_CRC64_ONE_WG) || (MODE == 2 && kCrc64OffTwo));
+    // 11-lookup fold: aligned batches at one workgroup per CU (0 = kFixedAligned)
+    static constexpr int fold = W == 64 && MODE == 0 && !two && MCK_CRC64_P6 && MCK_CRC64_FOLD11 ? kFold11 : kFold12;
+    static constexpr bool ops_global = W == 64 && MODE == 0 && fold == kFold12 && (MCK_CRC64_SPLIT || MCK_CRC64_P6) &&
+                                       !(MCK_CRC64_ONE_WG && MCK_CRC64_ONE_WG_OPS_LDS);
     static constexpr int block = LIGHT ? kLightBlock : two ? MCK_BLOCK64 : kBlock;
     static constexpr int blocks_per_cu = LIGHT ? 8 : two ? 2 : 1;
-    static constexpr int ops_mode = ops_global ? kOpsGlobal : (W == 64 && MODE == 2 && kCrc64OffMix) ? kOpsMix : kOpsLds;
-    static constexpr uint32_t lds64_bytes = ops_mode == kOpsGlobal ? kL64Main
-                                          : ops_mode == kOpsMix    ? kL64Main + 6 * 2048
-                                                                   : kL64Bytes;
+    static constexpr int ops_mode = ops_global                                              ? kOpsGlobal
+                                    : fold == kFold11 || (W == 64 && MODE == 2 && kCrc64OffMix) ? kOpsMix
+                                                                                              : kOpsLds;
+    static constexpr uint32_t lds64_bytes = fold == kFold11            ? kF11Bytes
+                                          : ops_mode == kOpsGlobal    ? kL64Main
+                                          : ops_mode == kOpsMix       ? kL64Main + 6 * 2048
+                                                                      : kL64Bytes;
 };
 // single-argument aliases (a comma inside __launch_bounds__ splits the macro)
 template <int MODE>
@@ -1483,6 +1525,19 @@ struct Lane64 {
     uint32_t al[4];
 };
 __device__ __forceinline__ Lane64 lane64(uint32_t lc) { return Lane64{lc, {lc, lc, lc, lc}}; }
+// kFold11: the lane-copy registers of the four 7-bit tables and the 6-bit
+// one, each with its 64 KiB region in byte 2
+struct Lane64F11 {
+    uint32_t a7[4];
+    uint32_t a6;
+};
+template <int FL>
+using LaneT = std::conditional_t<FL == kFold11, Lane64F11, Lane64>;
+template <int FL>
+__device__ __forceinline__ LaneT<FL> lane_regs(uint32_t lc) {
+    if constexpr (FL == kFold11) return Lane64F11{{lc, lc, lc | 0x10000u, lc | 0x10000u}, lc | 0x20000u};
+    else return lane64(lc);
+}
 
 #define MCK_SDWA_HI(B)                                                                              \
     __device__ __forceinline__ uint32_t sdwa_hi##B(uint32_t x) {                                    \
@@ -1620,6 +1675,62 @@ __device__ __forceinline__ uint64_t f64x(const uint8_t *lds, uint64_t x, uint64_
 }
 #endif
 
+#if MCK_CRC64_P6
+// (byte B of x) & 0x7F into byte 1 of the lane-copy register a (7-bit index).
+#define MCK_SDWA_P7(B)                                                                              \
+    __device__ __forceinline__ void sdwa_p7_##B(uint32_t &a, uint32_t x) {                          \
+        asm("v_and_b32_sdwa %0, %1, %2 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD "   \
+            "src1_sel:BYTE_" #B : "+v"(a) : "s"(0x7Fu), "v"(x));                                    \
+    }
+MCK_SDWA_P7(0)
+MCK_SDWA_P7(1)
+MCK_SDWA_P7(2)
+MCK_SDWA_P7(3)
+#undef MCK_SDWA_P7
+__device__ __forceinline__ uint32_t bfi32(uint32_t mask, uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(mask), "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ uint64_t xor12(const uint64_t *r, uint64_t extra) {
+    const uint64_t a = xor3_64(r[0], r[1], r[2]), b = xor3_64(r[3], r[4], r[5]), c = xor3_64(r[6], r[7], r[8]);
+    return xor3_64(a, b, c) ^ xor3_64(r[9], r[10], extra);
+}
+// Z^(16G)(x) ^ next in 11 lookups (kFold11 map above; the index formation is
+// restated in tests/native/kernel_emulator.cpp and checked there against the
+// nibble fold):
+//   f5[j]   bits 3..7 of byte j, j < 6          (byte & 0xF8: its own address)
+//   f7[0/1] bits 0..6 of byte 6 / 7
+//   t  = bfi(0x07070707, xl, xh << 3)           byte i: bits 0..2 of bytes i, i+4
+//   t2 = bfi(0x3F3F, t, xh >> 17)               + bit 7 of byte 6 / 7 at bit 6
+//   f7[2/3] byte 0 / 1 of t2 (7 bits)
+//   t3 = bfi(0x07070707, xl, xl >> 5)           byte 2: bits 0..2 of bytes 2, 3
+//   f6b     byte 2 of t3 (6 bits)
+__device__ __forceinline__ uint64_t f64x(const uint8_t *lds, uint64_t x, uint64_t next, Lane64F11 &ln) {
+    const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
+    uint64_t r[11];
+    r[0] = lds64(lds, sdwa_f8_0(xl) + kF11F5 + 0 * 256);
+    r[1] = lds64(lds, sdwa_f8_1(xl) + kF11F5 + 1 * 256);
+    r[2] = lds64(lds, sdwa_f8_2(xl) + kF11F5 + 2 * 256);
+    r[3] = lds64(lds, sdwa_f8_3(xl) + kF11F5 + 3 * 256);
+    r[4] = lds64(lds, sdwa_f8_0(xh) + kF11F5 + 4 * 256);
+    r[5] = lds64(lds, sdwa_f8_1(xh) + kF11F5 + 5 * 256);
+    sdwa_p7_2(ln.a7[0], xh);
+    r[6] = lds64(lds, ln.a7[0] + kF11F7a);
+    sdwa_p7_3(ln.a7[1], xh);
+    r[7] = lds64(lds, ln.a7[1] + kF11F7a + 32768);
+    const uint32_t t2 = bfi32(0x3F3Fu, gather6(xl, xh), xh >> 17);
+    sdwa_p7_0(ln.a7[2], t2);
+    r[8] = lds64(lds, ln.a7[2] + (kF11F7c - 65536));
+    sdwa_p7_1(ln.a7[3], t2);
+    r[9] = lds64(lds, ln.a7[3] + (kF11F7c - 65536 + 32768));
+    const uint32_t t3 = bfi32(0x07070707u, xl, xl >> 5);
+    sdwa_p6_2(ln.a6, t3);
+    r[10] = lds64(lds, ln.a6 + (kF11F6 - 131072));
+    return xor12(r, next);
+}
+#endif
+
 template <bool OG>
 __device__ __forceinline__ uint64_t op64(const uint8_t *lds, const crc64_gpu_pack_t *pk, uint32_t o, uint64_t x) {
     uint64_t r[16];
@@ -1659,10 +1770,30 @@ __device__ __forceinline__ uint64_t combine64(const uint8_t *lds, const crc64_gp
     return x;
 }
 
-template <int BLOCK, int OM>
+template <int BLOCK, int OM, int FL = kFold12>
 __device__ void fill_lds64(uint8_t *lds, const crc64_gpu_pack_t *pk) {
     uint64_t *l = reinterpret_cast<uint64_t *>(lds);
     uint4 *l4 = reinterpret_cast<uint4 *>(lds);
+    if constexpr (FL == kFold11) {
+        static_assert(OM != kOpsLds, "the 11-lookup map holds the butterfly operators only");
+        // f7: entry v of table i at region_i + v*256 B, 32 copies (two per 16-B write)
+        for (uint32_t q = threadIdx.x; q < 4u * 128u * 16u; q += BLOCK) {
+            const uint32_t i = q >> 11, v = (q >> 4) & 127u;
+            const uint64_t e = pk->f7[i][v];
+            const uint32_t base = i < 2 ? kF11F7a + i * 32768u : kF11F7c + (i - 2) * 32768u;
+            l4[(base >> 4) + (v << 4) + (q & 15u)] = make_uint4((uint32_t)e, (uint32_t)(e >> 32), (uint32_t)e, (uint32_t)(e >> 32));
+        }
+        for (uint32_t q = threadIdx.x; q < 64u * 16u; q += BLOCK) {
+            const uint64_t e = pk->f6b[q >> 4];
+            l4[kF11F6 / 16 + q] = make_uint4((uint32_t)e, (uint32_t)(e >> 32), (uint32_t)e, (uint32_t)(e >> 32));
+        }
+        for (uint32_t d = threadIdx.x; d < 6u * 32u; d += BLOCK) l[kF11F5 / 8 + d] = pk->f5[d >> 5][d & 31u];
+        if constexpr (OM == kOpsMix) {  // ops 1..6 at kL64Main
+            const uint4 *ops = reinterpret_cast<const uint4 *>(&pk->ops[1][0][0]);
+            for (uint32_t q = threadIdx.x; q < 6u * 128u; q += BLOCK) l4[kL64Main / 16 + q] = ops[q];
+        }
+        return;
+    }
 #if MCK_CRC64_P6
     // f6: entry v of table i at i*16 KiB + v*256 B, 32 copies (two per 16-B write)
     for (uint32_t q = threadIdx.x; q < 4096u; q += BLOCK) {
@@ -1711,12 +1842,12 @@ __device__ __forceinline__ uint64_t hi64(uint4 v) { return (uint64_t)v.w << 32 |
 #ifndef MCK_A64_EVEN
 #define MCK_A64_EVEN 1
 #endif
-template <int LOG2G, bool NT, bool OG>
+template <int LOG2G, bool NT, int OM, int FL = kFold12>
 __device__ __forceinline__ uint64_t payload64_even(const uint8_t *lds, const crc64_gpu_pack_t *pk, const uint8_t *p,
                                                    uint32_t K, uint32_t gl, uint32_t lc, uint64_t init) {
     constexpr int G = 1 << LOG2G;
     constexpr int R = NT ? MCK_RING64_NT : MCK_RING64;
-    Lane64 ln = lane64(lc);
+    LaneT<FL> ln = lane_regs<FL>(lc);
     gbyte_t src = global_ptr(p, LOG2G == 6) + 16u * gl;
     uint4 ring[R];
 #pragma unroll
@@ -1739,17 +1870,17 @@ __device__ __forceinline__ uint64_t payload64_even(const uint8_t *lds, const crc
         x0 = f64x(lds, x0, lo64(nx), ln);
         x1 = f64x(lds, x1, hi64(nx), ln);
     }
-    return combine64<LOG2G, OG>(lds, pk, x0, x1, gl);
+    return combine64<LOG2G, OM>(lds, pk, x0, x1, gl);
 }
 
-template <int LOG2G, bool NT, bool OG>
+template <int LOG2G, bool NT, int OM, int FL = kFold12>
 __device__ __forceinline__ uint64_t payload64_aligned(const uint8_t *lds, const crc64_gpu_pack_t *pk, const uint8_t *p,
                                                       uint32_t K, uint32_t gl, uint32_t lc, uint64_t init) {
     constexpr int G = 1 << LOG2G;
     constexpr int R = NT ? MCK_RING64_NT : MCK_RING64;
     if (MCK_A64_EVEN && MCK_LA64 && K % R == 0 && K >= 2 * R)
-        return payload64_even<LOG2G, NT, OG>(lds, pk, p, K, gl, lc, init);
-    Lane64 ln = lane64(lc);
+        return payload64_even<LOG2G, NT, OM, FL>(lds, pk, p, K, gl, lc, init);
+    LaneT<FL> ln = lane_regs<FL>(lc);
     // global (address-space 1) loads: a flat load would also hold up every LDS wait
     const gbyte_t src = global_ptr(p, LOG2G == 6) + 16u * gl;
     auto ldk = [&](uint32_t k) { return ldg16<NT>(src + (uint64_t)k * (16u * G)); };
@@ -1795,7 +1926,7 @@ __device__ __forceinline__ uint64_t payload64_aligned(const uint8_t *lds, const 
         }
     }
 #endif
-    return combine64<LOG2G, OG>(lds, pk, x0, x1, gl);
+    return combine64<LOG2G, OM>(lds, pk, x0, x1, gl);
 }
 
 template <int LOG2G, bool NT, int OM = kOpsLds>
@@ -1868,7 +1999,7 @@ __device__ __forceinline__ uint64_t tail64(const uint8_t *lds, const crc64_gpu_p
 }
 
 // CRC-64 counterpart of payload32_g64 (a non-zero RAW `reg` needs len >= 8).
-template <bool NT, bool RAW = false, int OM = kOpsLds>
+template <bool NT, bool RAW = false, int OM = kOpsLds, int FL = kFold12>
 __device__ __forceinline__ uint64_t payload64_g64(const uint8_t *lds, const crc64_gpu_pack_t *pk, const uint8_t *p,
                                                   uint64_t len, uint32_t gl, uint32_t lc, uint64_t reg = 0ull) {
     const uint64_t init = RAW ? reg : pk->init;
@@ -1887,7 +2018,7 @@ __device__ __forceinline__ uint64_t payload64_g64(const uint8_t *lds, const crc6
     constexpr uint32_t R = kRingOff64;
 
     uint64_t x0 = 0, x1 = 0;
-    Lane64 ln = lane64(lc);
+    LaneT<FL> ln = lane_regs<FL>(lc);
     auto fold = [&](uint32_t kk, uint4 v) {
         uint64_t w0 = lo64(v), w1 = hi64(v);
         if (kk < kc0 || kk >= kc1) {  // wave-uniform: an edge step
@@ -1951,7 +2082,7 @@ __global__ __launch_bounds__(kBlk64<MODE>, kWpe64<MODE>) void crc64_batch_kernel
         sacc[threadIdx.x] = 0;
         scnt[threadIdx.x] = 0;
     }
-    fill_lds64<S::block, S::ops_mode>(lds, pk);
+    fill_lds64<S::block, S::ops_mode, S::fold>(lds, pk);
     __syncthreads();
     MCK_STAMP(blockIdx.x * kWPB + (threadIdx.x >> 6), 1);
 
@@ -2003,7 +2134,7 @@ __global__ __launch_bounds__(kBlk64<MODE>, kWpe64<MODE>) void crc64_batch_kernel
             for_each_unit<true, false, true>(&wgq, a.queue, units, wave, nw, [&](uint64_t u, uint32_t r) {
                 const uint64_t p = u >> sl;
                 const uint32_t q = (uint32_t)u & (pieces - 1);
-                const uint64_t x = payload64_aligned<6, NT, S::ops_global>(
+                const uint64_t x = payload64_aligned<6, NT, S::ops_mode, S::fold>(
                     lds, pk, a.base + p * a.stride + (uint64_t)q * kSplitBytes, (uint32_t)(kSplitBytes >> 10), gl, lc,
                     q == 0 ? pk->init : 0ull);
                 if (gl == 0) {
@@ -2031,8 +2162,8 @@ __global__ __launch_bounds__(kBlk64<MODE>, kWpe64<MODE>) void crc64_batch_kernel
         const bool act = p < a.count;
         const uint64_t pc = act ? p : a.count - 1;
         uint64_t x;
-        if (MODE == kFixedAligned)
-            x = payload64_aligned<LOG2G, NT, S::ops_global>(lds, pk, a.base + pc * a.stride, (uint32_t)(a.len >> (4 + LOG2G)), gl, lc, pk->init);
+        if constexpr (MODE == kFixedAligned)
+            x = payload64_aligned<LOG2G, NT, S::ops_mode, S::fold>(lds, pk, a.base + pc * a.stride, (uint32_t)(a.len >> (4 + LOG2G)), gl, lc, pk->init);
         else
             x = payload64_generic<LOG2G, NT>(lds, pk, a.base + pc * a.stride, a.len, gl, lc);
         if (act && gl == 0) emit<uint64_t, VERIFY>(a, p, x ^ xorout);
