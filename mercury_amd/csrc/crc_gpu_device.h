@@ -101,7 +101,23 @@ constexpr uint32_t kL64Bytes = kL64Main + CRC64_NOPS_MAX * 2048;
 //   [145408, 161792)   f6b (x32)
 // An address is the lane-copy register (byte 0: copy offset, byte 1: the
 // index, byte 2: the 64 KiB region) plus the DS immediate offset (< 64 KiB).
-enum Fold : int { kFold12 = 0, kFold11 = 1 };
+enum Fold : int { kFold12 = 0, kFold11 = 1, kFold12W = 2 };
+// kFold12W (round 5): the 12-lookup fold with its addresses formed by ops that
+// issue in ~1.8 cycles (VOP2 AND / v_bitop3 with VGPR operands) instead of
+// SDWA (~2.8; tools/valu_probe.hip).  Bits 3..7 of the even bytes of each
+// half stay in unreplicated 256-B tables (address = x & 0xF8 after a 16-bit
+// shift for bytes 2 and 6); bits 3..7 of the odd bytes are read in place as
+// (x & 0xF800) | lane copy -- entry v at v * 2 KiB, so these four tables are
+// replicated 32x in rows of 2 KiB, interleaved (slot k at +256 k); the pair
+// index of t's byte 1 is (t & 0x3F00) | lane copy, the other three stay SDWA.
+//   [0, 65536)        rows v = 0..31 of 2 KiB: slots 0..3 = f5[1], f5[3],
+//                     f5[5], f5[7] (x32); [1024, 2048) of row 0: f5[0, 2, 4, 6]
+//   [67584, 79872)    butterfly operators (kL64Main, the mixed operator mode)
+//   [79872, 145408)   f6[0..3] (x32), region 1 of the lane registers
+constexpr uint32_t kWUnrep = 1024;
+constexpr uint32_t kWF6 = kL64Main + 6 * 2048;
+constexpr uint32_t kWBytes = kWF6 + 4 * 16384;
+static_assert(kWF6 - 65536 + 3 * 16384 < 65536, "f6 offsets fit the DS immediate");
 constexpr uint32_t kF11F5 = 512;
 constexpr uint32_t kF11F7a = 2048;
 constexpr uint32_t kF11F7c = kL64Main + 6 * 2048;
@@ -184,19 +200,34 @@ enum OpsMode : int { kOpsLds = 0, kOpsGlobal = 1, kOpsMix = 2 };
 #ifndef MCK_CRC64_FOLD11
 #define MCK_CRC64_FOLD11 0
 #endif
+// MCK_CRC64_TWO_MIX=1 (with MCK_CRC64_ONE_WG=0): the two-workgroup aligned
+// kernels keep the butterfly operators in LDS (mixed mode, 79.9 KiB each).
+#ifndef MCK_CRC64_TWO_MIX
+#define MCK_CRC64_TWO_MIX 0
+#endif
+#ifndef MCK_CRC64_FOLD12W
+#define MCK_CRC64_FOLD12W 0
+#endif
 template <int W, int MODE, bool LIGHT = false>
 struct Shape {
     static constexpr bool two = W == 64 && ((MODE == 0 && !MCK_CRC64_ONE_WG) || (MODE == 2 && kCrc64OffTwo));
-    // 11-lookup fold: aligned batches at one workgroup per CU (0 = kFixedAligned)
-    static constexpr int fold = W == 64 && MODE == 0 && !two && MCK_CRC64_P6 && MCK_CRC64_FOLD11 ? kFold11 : kFold12;
+    // aligned batches at one workgroup per CU (0 = kFixedAligned): the 11-lookup
+    // or the wide-row fold
+    static constexpr bool one_wg_aligned = W == 64 && MODE == 0 && !two && MCK_CRC64_P6;
+    static constexpr int fold = one_wg_aligned && MCK_CRC64_FOLD11    ? kFold11
+                                : one_wg_aligned && MCK_CRC64_FOLD12W ? kFold12W
+                                                                      : kFold12;
     static constexpr bool ops_global = W == 64 && MODE == 0 && fold == kFold12 && (MCK_CRC64_SPLIT || MCK_CRC64_P6) &&
-                                       !(MCK_CRC64_ONE_WG && MCK_CRC64_ONE_WG_OPS_LDS);
+                                       !(MCK_CRC64_ONE_WG && MCK_CRC64_ONE_WG_OPS_LDS) && !MCK_CRC64_TWO_MIX;
     static constexpr int block = LIGHT ? kLightBlock : two ? MCK_BLOCK64 : kBlock;
     static constexpr int blocks_per_cu = LIGHT ? 8 : two ? 2 : 1;
-    static constexpr int ops_mode = ops_global                                              ? kOpsGlobal
-                                    : fold == kFold11 || (W == 64 && MODE == 2 && kCrc64OffMix) ? kOpsMix
-                                                                                              : kOpsLds;
+    static constexpr int ops_mode = ops_global ? kOpsGlobal
+                                    : fold != kFold12 || (W == 64 && MODE == 2 && kCrc64OffMix) ||
+                                              (W == 64 && MODE == 0 && two && MCK_CRC64_TWO_MIX)
+                                          ? kOpsMix
+                                          : kOpsLds;
     static constexpr uint32_t lds64_bytes = fold == kFold11            ? kF11Bytes
+                                          : fold == kFold12W          ? kWBytes
                                           : ops_mode == kOpsGlobal    ? kL64Main
                                           : ops_mode == kOpsMix       ? kL64Main + 6 * 2048
                                                                       : kL64Bytes;
@@ -1531,12 +1562,30 @@ struct Lane64F11 {
     uint32_t a7[4];
     uint32_t a6;
 };
+// kFold12W: the lane copy (plain and with region 1), the three SDWA pair
+// registers (region 1) and the masks, all in VGPRs (an SGPR operand costs a
+// VALU op ~1 cycle more)
+struct Lane64W {
+    uint32_t lc, lcr, al0, al2, al3;
+    uint32_t m8, mF800, m3F00, m07;
+};
 template <int FL>
-using LaneT = std::conditional_t<FL == kFold11, Lane64F11, Lane64>;
+using LaneT = std::conditional_t<FL == kFold11, Lane64F11, std::conditional_t<FL == kFold12W, Lane64W, Lane64>>;
+__device__ __forceinline__ uint32_t vmov(uint32_t m) {
+    uint32_t r;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "s"(m));
+    return r;
+}
 template <int FL>
 __device__ __forceinline__ LaneT<FL> lane_regs(uint32_t lc) {
-    if constexpr (FL == kFold11) return Lane64F11{{lc, lc, lc | 0x10000u, lc | 0x10000u}, lc | 0x20000u};
-    else return lane64(lc);
+    if constexpr (FL == kFold11) {
+        return Lane64F11{{lc, lc, lc | 0x10000u, lc | 0x10000u}, lc | 0x20000u};
+    } else if constexpr (FL == kFold12W) {
+        const uint32_t r1 = lc | 0x10000u;
+        return Lane64W{lc, r1, r1, r1, r1, vmov(0xF8u), vmov(0xF800u), vmov(0x3F00u), vmov(0x07070707u)};
+    } else {
+        return lane64(lc);
+    }
 }
 
 #define MCK_SDWA_HI(B)                                                                              \
@@ -1624,8 +1673,32 @@ MCK_SDWA_P6(3)
 #ifndef MCK_BFI64
 #define MCK_BFI64 1
 #endif
+// Round 5 (tools/valu_probe.hip, profiles/r05/valu_probe.txt): on gfx950 a
+// wave64 v_bitop3_b32 / v_and_b32 / v_xor_b32 with VGPR operands issues in
+// ~1.8 shader cycles per SIMD (4 waves/SIMD), v_bfi_b32, v_perm_b32, every
+// SDWA form and any VALU op with an SGPR operand in ~2.8.  MCK_CHEAP64=1: the
+// bit-select as a v_bitop3 (S0 ? S1 : S2 = 0xCA) with its mask in a VGPR, and
+// byte 0's f5 address as a VOP2 AND with a VGPR mask, instead of v_bfi_b32 and
+// an SDWA AND with the mask in SGPRs.
+#ifndef MCK_CHEAP64
+#define MCK_CHEAP64 0
+#endif
+__device__ __forceinline__ uint32_t vmask(uint32_t m) {
+    uint32_t r;
+    asm("v_mov_b32 %0, %1" : "=v"(r) : "s"(m));  // loop-invariant: hoisted by the compiler
+    return r;
+}
+__device__ __forceinline__ uint32_t and_v(uint32_t x, uint32_t mv) {
+    uint32_t r;
+    asm("v_and_b32 %0, %1, %2" : "=v"(r) : "v"(mv), "v"(x));
+    return r;
+}
 __device__ __forceinline__ uint32_t gather6(uint32_t xl, uint32_t xh) {
-#if MCK_BFI64
+#if MCK_BFI64 && MCK_CHEAP64
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xca" : "=v"(r) : "v"(vmask(0x07070707u)), "v"(xl), "v"(xh << 3));
+    return r;
+#elif MCK_BFI64
     uint32_t r;
     asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(0x07070707u), "v"(xl), "v"(xh << 3));
     return r;
@@ -1643,11 +1716,20 @@ __device__ __forceinline__ uint64_t f64x(const uint8_t *lds, uint64_t x, uint64_
     // byte i of t: bits 0..2 of bytes i and i + 4 of the word (bit-select)
     const uint32_t t = gather6(xl, xh);
     uint64_t r[12];
+#if MCK_CHEAP64
+    const uint32_t m8 = vmask(0xF8u);
+    r[0] = lds64(lds, and_v(xl, m8) + kL64P5 + 0 * 256);
+#else
     r[0] = lds64(lds, sdwa_f8_0(xl) + kL64P5 + 0 * 256);
+#endif
     r[1] = lds64(lds, sdwa_f8_1(xl) + kL64P5 + 1 * 256);
     r[2] = lds64(lds, sdwa_f8_2(xl) + kL64P5 + 2 * 256);
     r[3] = lds64(lds, sdwa_f8_3(xl) + kL64P5 + 3 * 256);
+#if MCK_CHEAP64
+    r[4] = lds64(lds, and_v(xh, m8) + kL64P5 + 4 * 256);
+#else
     r[4] = lds64(lds, sdwa_f8_0(xh) + kL64P5 + 4 * 256);
+#endif
     r[5] = lds64(lds, sdwa_f8_1(xh) + kL64P5 + 5 * 256);
     r[6] = lds64(lds, sdwa_f8_2(xh) + kL64P5 + 6 * 256);
     r[7] = lds64(lds, sdwa_f8_3(xh) + kL64P5 + 7 * 256);
@@ -1676,6 +1758,42 @@ __device__ __forceinline__ uint64_t f64x(const uint8_t *lds, uint64_t x, uint64_
 #endif
 
 #if MCK_CRC64_P6
+// (x & m) | c in one v_bitop3 (truth table 0xEA), every operand a VGPR
+__device__ __forceinline__ uint32_t andor3(uint32_t x, uint32_t m, uint32_t c) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xea" : "=v"(r) : "v"(x), "v"(m), "v"(c));
+    return r;
+}
+// s ? a : b bitwise in one v_bitop3 (0xCA), every operand a VGPR
+__device__ __forceinline__ uint32_t sel3(uint32_t s, uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xca" : "=v"(r) : "v"(s), "v"(a), "v"(b));
+    return r;
+}
+// Z^(16G)(x) ^ next, the 12 lookups of the pack's f5 / f6 tables in the
+// kFold12W map (above): 9 address ops at ~1.8 cycles + 3 SDWA instead of 12 SDWA.
+__device__ __forceinline__ uint64_t f64x(const uint8_t *lds, uint64_t x, uint64_t next, Lane64W &ln) {
+    const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
+    const uint32_t yl = xl >> 16, yh = xh >> 16;
+    uint64_t r[12];
+    r[0] = lds64(lds, and_v(xl, ln.m8) + kWUnrep + 0 * 256);
+    r[1] = lds64(lds, andor3(xl, ln.mF800, ln.lc) + 0 * 256);
+    r[2] = lds64(lds, and_v(yl, ln.m8) + kWUnrep + 1 * 256);
+    r[3] = lds64(lds, andor3(yl, ln.mF800, ln.lc) + 1 * 256);
+    r[4] = lds64(lds, and_v(xh, ln.m8) + kWUnrep + 2 * 256);
+    r[5] = lds64(lds, andor3(xh, ln.mF800, ln.lc) + 2 * 256);
+    r[6] = lds64(lds, and_v(yh, ln.m8) + kWUnrep + 3 * 256);
+    r[7] = lds64(lds, andor3(yh, ln.mF800, ln.lc) + 3 * 256);
+    const uint32_t t = sel3(ln.m07, xl, xh << 3);
+    sdwa_p6_0(ln.al0, t);
+    r[8] = lds64(lds, ln.al0 + (kWF6 - 65536) + 0 * 16384);
+    r[9] = lds64(lds, andor3(t, ln.m3F00, ln.lcr) + (kWF6 - 65536) + 1 * 16384);
+    sdwa_p6_2(ln.al2, t);
+    r[10] = lds64(lds, ln.al2 + (kWF6 - 65536) + 2 * 16384);
+    sdwa_p6_3(ln.al3, t);
+    r[11] = lds64(lds, ln.al3 + (kWF6 - 65536) + 3 * 16384);
+    return xor13(r, next);
+}
 // (byte B of x) & 0x7F into byte 1 of the lane-copy register a (7-bit index).
 #define MCK_SDWA_P7(B)                                                                              \
     __device__ __forceinline__ void sdwa_p7_##B(uint32_t &a, uint32_t x) {                          \
@@ -1774,6 +1892,26 @@ template <int BLOCK, int OM, int FL = kFold12>
 __device__ void fill_lds64(uint8_t *lds, const crc64_gpu_pack_t *pk) {
     uint64_t *l = reinterpret_cast<uint64_t *>(lds);
     uint4 *l4 = reinterpret_cast<uint4 *>(lds);
+    if constexpr (FL == kFold12W) {
+        static_assert(OM != kOpsLds, "the wide-row map holds the butterfly operators only");
+        // odd-byte f5 tables: entry v of slot k (f5[2k + 1]) at v * 2048 + k * 256, 32 copies
+        for (uint32_t q = threadIdx.x; q < 4u * 32u * 16u; q += BLOCK) {
+            const uint32_t k = q >> 9, v = (q >> 4) & 31u;
+            const uint64_t e = pk->f5[2 * k + 1][v];
+            l4[v * 128u + k * 16u + (q & 15u)] = make_uint4((uint32_t)e, (uint32_t)(e >> 32), (uint32_t)e, (uint32_t)(e >> 32));
+        }
+        for (uint32_t d = threadIdx.x; d < 4u * 32u; d += BLOCK) l[kWUnrep / 8 + d] = pk->f5[2 * (d >> 5)][d & 31u];
+        // f6: entry v of table i at kWF6 + i * 16 KiB + v * 256 B, 32 copies
+        for (uint32_t q = threadIdx.x; q < 4096u; q += BLOCK) {
+            const uint64_t v = pk->f6[q >> 10][(q >> 4) & 63u];
+            l4[kWF6 / 16 + q] = make_uint4((uint32_t)v, (uint32_t)(v >> 32), (uint32_t)v, (uint32_t)(v >> 32));
+        }
+        if constexpr (OM == kOpsMix) {  // ops 1..6 at kL64Main
+            const uint4 *ops = reinterpret_cast<const uint4 *>(&pk->ops[1][0][0]);
+            for (uint32_t q = threadIdx.x; q < 6u * 128u; q += BLOCK) l4[kL64Main / 16 + q] = ops[q];
+        }
+        return;
+    }
     if constexpr (FL == kFold11) {
         static_assert(OM != kOpsLds, "the 11-lookup map holds the butterfly operators only");
         // f7: entry v of table i at region_i + v*256 B, 32 copies (two per 16-B write)
