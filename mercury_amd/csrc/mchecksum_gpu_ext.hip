@@ -106,24 +106,28 @@ constexpr uint32_t kDescWords = 8;  // per scan block: flag, aggregate (p, c, r)
 
 __device__ __forceinline__ uint64_t seg_chunks(uint64_t l) { return (l + kChunk - 1) / kChunk; }
 
-// Block-wide inclusive scan of (p, c) over 256 threads; returns the block
+// Block-wide inclusive scan of (p, c) over the first 256 threads (a wider
+// block's other threads only take part in the barrier); returns the block
 // totals through *tp, *tc.
 __device__ __forceinline__ void block_scan2(uint64_t &p, uint64_t &c, uint64_t *tp, uint64_t *tc) {
     __shared__ uint64_t wp[4], wc[4];
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    if (w < kScanThreads / 64) {
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint64_t op = __shfl_up(p, d, 64), oc = __shfl_up(c, d, 64);
-        if (lane >= (uint32_t)d) {
-            p += op;
-            c += oc;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t op = __shfl_up(p, d, 64), oc = __shfl_up(c, d, 64);
+            if (lane >= (uint32_t)d) {
+                p += op;
+                c += oc;
+            }
+        }
+        if (lane == 63) {
+            wp[w] = p;
+            wc[w] = c;
         }
     }
-    if (lane == 63) {
-        wp[w] = p;
-        wc[w] = c;
-    }
     __syncthreads();
+    if (w >= kScanThreads / 64) return;
     uint64_t bp = 0, bc = 0, sp = 0, sc = 0;
 #pragma unroll
     for (uint32_t v = 0; v < kScanThreads / 64; v++) {
@@ -260,81 +264,105 @@ __device__ __forceinline__ bool seg_lookback(uint64_t *desc, uint64_t b, uint64_
 // starts at or before it), and every thread then reads its own segments'
 // entries.  Round 3 ran a binary search over all of first[] in global memory
 // per segment: ~14 dependent loads, 15 of the pass's 17 us at 32768 segments.
-__global__ __launch_bounds__(kScanThreads) void seg_scan(const uint64_t *len, const uint64_t *addr, uint64_t nseg,
-                                                         uint64_t *desc, uint64_t epoch, uint64_t *P, uint64_t *C,
-                                                         unsigned long long *ragged, const uint64_t *first,
-                                                         uint64_t nobj, uint64_t *obj, uint32_t *map, uint64_t map_cap,
-                                                         void *out, uint32_t width, uint64_t preset,
-                                                         uint32_t *err_word, uint64_t fault_block) {
-    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-    const uint64_t b = blockIdx.x, nb = gridDim.x;
+// The scan's arguments (one launch, or block 0 of a fused chunk pass).
+struct ScanArgs {
+    const uint64_t *len, *addr;
+    uint64_t nseg;
+    uint64_t *desc;
+    uint64_t epoch;
+    uint64_t *P, *C;
+    unsigned long long *ragged;
+    const uint64_t *first;
+    uint64_t nobj;
+    uint64_t *obj;
+    uint32_t *map;
+    uint64_t map_cap;
+    void *out;
+    uint32_t width;
+    uint64_t preset;
+    uint32_t *err_word;
+    uint64_t fault_block;
+};
+// LDS scratch of one scan block: the object rows of its segments (4 x u64 +
+// u32 each) and a few broadcast words
+constexpr uint32_t kScanScratch = kScanBlk * (4 * 8 + 4) + 64;
+
+// Scan block b of nb.  Threads below kScanThreads do the work; a wider block
+// (the fused chunk pass, 1024 threads) only joins the barriers with the rest.
+__device__ __forceinline__ void scan_block(const ScanArgs &sa, uint64_t b, uint64_t nb, uint8_t *scratch) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+    const bool act = tid < kScanThreads;
+    const uint64_t nseg = sa.nseg, nobj = sa.nobj;
     const uint64_t s0 = b * kScanBlk, s1 = s0 + kScanBlk < nseg ? s0 + kScanBlk : nseg;
+    uint64_t *row = reinterpret_cast<uint64_t *>(scratch);
+    uint64_t *row_f0 = row + kScanBlk, *row_f1 = row_f0 + kScanBlk;  // the object's first[j], first[j + 1]
+    uint64_t *row_hs = row_f1 + kScanBlk;                             // the object's head segment
+    uint32_t *row_ne = reinterpret_cast<uint32_t *>(row_hs + kScanBlk);  // 1: the segment is not empty
+    uint64_t *bc = reinterpret_cast<uint64_t *>(row_ne + kScanBlk);     // jb, je, ex[3]
+    uint32_t *rag = reinterpret_cast<uint32_t *>(bc + 5);
     // every object starts as the CRC of the empty message (the chunk passes XOR into it)
-    for (uint64_t j = b * kScanThreads + threadIdx.x; j < nobj; j += nb * kScanThreads) {
-        if (width == 64) reinterpret_cast<uint64_t *>(out)[j] = preset;
-        else reinterpret_cast<uint32_t *>(out)[j] = (uint32_t)preset;
-    }
+    if (act)
+        for (uint64_t j = b * kScanThreads + tid; j < nobj; j += nb * kScanThreads) {
+            if (sa.width == 64) reinterpret_cast<uint64_t *>(sa.out)[j] = sa.preset;
+            else reinterpret_cast<uint32_t *>(sa.out)[j] = (uint32_t)sa.preset;
+        }
     uint64_t l[kScanPer], p = 0, c = 0, r = 0;
 #pragma unroll
     for (uint32_t e = 0; e < kScanPer; e++) {
-        const uint64_t i = s0 + threadIdx.x * kScanPer + e;
-        l[e] = i < nseg ? len[i] : 0;
+        const uint64_t i = s0 + tid * kScanPer + e;
+        l[e] = act && i < nseg ? sa.len[i] : 0;
         p += l[e];
         c += seg_chunks(l[e]);
-        r |= i < nseg && l[e] && (l[e] % 1024 != 0 || addr[i] % 16 != 0);
+        r |= act && i < nseg && l[e] && (l[e] % 1024 != 0 || sa.addr[i] % 16 != 0);
     }
     // the objects touching this block (queue pass only)
-    const uint64_t f0 = first[0], f1 = first[nobj];
+    const uint64_t f0 = sa.first[0], f1 = sa.first[nobj];
     const uint64_t lo_s = s0 > f0 ? s0 : f0, hi_s = s1 < f1 ? s1 : f1;
-    __shared__ uint64_t jb_s, je_s;
-    if (obj && lo_s < hi_s) {
+    if (sa.obj && lo_s < hi_s) {
         if (w == 1) {
-            const uint64_t jb = wave_last_le(first, nobj + 1, lo_s, lane);
-            if (lane == 0) jb_s = jb;
+            const uint64_t jb = wave_last_le(sa.first, nobj + 1, lo_s, lane);
+            if (lane == 0) bc[0] = jb;
         } else if (w == 2) {
-            const uint64_t je = wave_last_le(first, nobj + 1, hi_s - 1, lane);
-            if (lane == 0) je_s = je;
+            const uint64_t je = wave_last_le(sa.first, nobj + 1, hi_s - 1, lane);
+            if (lane == 0) bc[1] = je;
         }
     }
     const uint64_t p0 = p, c0 = c;
-    uint64_t tp, tc;
+    uint64_t tp = 0, tc = 0;
     block_scan2(p, c, &tp, &tc);
-    __shared__ uint32_t rag;
-    if (threadIdx.x == 0) rag = 0;
+    if (tid == 0) *rag = 0;
     __syncthreads();
-    if (__any(r != 0) && lane == 0) atomicOr(&rag, 1u);
+    if (act && __any(r != 0) && lane == 0) atomicOr(rag, 1u);
     __syncthreads();
-    __shared__ uint64_t ex[3];
+    uint64_t *ex = bc + 2;
     if (w == 0) {
         uint64_t ep, ec, er;
-        const bool ok = seg_lookback(desc, b, epoch, tp, tc, rag, lane, &ep, &ec, &er, fault_block);
+        const bool ok = seg_lookback(sa.desc, b, sa.epoch, tp, tc, *rag, lane, &ep, &ec, &er, sa.fault_block);
         if (lane == 0) {
             ex[0] = ep;
             ex[1] = ec;
             ex[2] = er;
-            if (!ok && err_word) atomicAdd(err_word, 1u);  // fail closed: the scan is not trustworthy
+            if (!ok && sa.err_word) atomicAdd(sa.err_word, 1u);  // fail closed: the scan is not trustworthy
         }
     }
     __syncthreads();
-    if (b + 1 == nb && threadIdx.x == 0) {
-        P[nseg] = ex[0] + tp;
-        C[nseg] = ex[1] + tc;
-        *ragged = ex[2] | rag;
+    if (b + 1 == nb && tid == 0) {
+        sa.P[nseg] = ex[0] + tp;
+        sa.C[nseg] = ex[1] + tc;
+        *sa.ragged = ex[2] | *rag;
     }
     uint64_t ep = ex[0] + p - p0, ec = ex[1] + c - c0;
-    __shared__ uint64_t row[kScanBlk];
-    __shared__ uint64_t row_f0[kScanBlk], row_f1[kScanBlk];  // the object's first[j], first[j + 1]
-    __shared__ uint64_t row_hs[kScanBlk];                      // the object's head segment
-    __shared__ uint32_t row_ne[kScanBlk];                      // 1: the segment is not empty
-    if (obj) {
-        for (uint32_t t = threadIdx.x; t < kScanBlk; t += kScanThreads) row[t] = kNoObj;
+    if (sa.obj) {
+        if (act) {
+            for (uint32_t t = tid; t < kScanBlk; t += kScanThreads) row[t] = kNoObj;
 #pragma unroll
-        for (uint32_t e = 0; e < kScanPer; e++) row_ne[threadIdx.x * kScanPer + e] = l[e] != 0;
+            for (uint32_t e = 0; e < kScanPer; e++) row_ne[tid * kScanPer + e] = l[e] != 0;
+        }
         __syncthreads();
-        if (lo_s < hi_s) {
-            const uint64_t jb = jb_s, je = je_s;
-            for (uint64_t k = jb + threadIdx.x; k <= je; k += kScanThreads) {
-                const uint64_t a0 = first[k], a1 = first[k + 1];
+        if (act && lo_s < hi_s) {
+            const uint64_t jb = bc[0], je = bc[1];
+            for (uint64_t k = jb + tid; k <= je; k += kScanThreads) {
+                const uint64_t a0 = sa.first[k], a1 = sa.first[k + 1];
                 const uint64_t lo = a0 > lo_s ? a0 : lo_s, hi = a1 < hi_s ? a1 : hi_s;
                 // the head segment is known here when the object starts in this
                 // block and one of its segments here is not empty; otherwise
@@ -356,30 +384,70 @@ __global__ __launch_bounds__(kScanThreads) void seg_scan(const uint64_t *len, co
         }
         __syncthreads();
     }
+    if (!act) return;
 #pragma unroll
     for (uint32_t e = 0; e < kScanPer; e++) {
-        const uint64_t i = s0 + threadIdx.x * kScanPer + e;
+        const uint64_t i = s0 + tid * kScanPer + e;
         if (i < nseg) {
-            P[i] = ep;
-            C[i] = ec;
-            if (obj) {
+            sa.P[i] = ep;
+            sa.C[i] = ec;
+            if (sa.obj) {
                 const uint64_t t = i - s0;
-                obj[4 * i] = row[t];
+                sa.obj[4 * i] = row[t];
                 if (row[t] != kNoObj) {
-                    obj[4 * i + 1] = row_f0[t];
-                    obj[4 * i + 2] = row_f1[t];
-                    obj[4 * i + 3] = row_hs[t];
+                    sa.obj[4 * i + 1] = row_f0[t];
+                    sa.obj[4 * i + 2] = row_f1[t];
+                    sa.obj[4 * i + 3] = row_hs[t];
                 }
             }
             // chunk -> segment map, while it fits (the chunk passes check the
             // total against map_cap and search C otherwise)
             const uint64_t ce = ec + seg_chunks(l[e]);
-            if (ce <= map_cap)
-                for (uint64_t k = ec; k < ce; k++) map[k] = (uint32_t)i;
+            if (ce <= sa.map_cap)
+                for (uint64_t k = ec; k < ce; k++) sa.map[k] = (uint32_t)i;
         }
         ep += l[e];
         ec += seg_chunks(l[e]);
     }
+}
+
+__global__ __launch_bounds__(kScanThreads) void seg_scan(ScanArgs sa) {
+    __shared__ __attribute__((aligned(16))) uint8_t scratch[kScanScratch];
+    scan_block(sa, blockIdx.x, gridDim.x, scratch);
+}
+
+// Fused scan (lists of one scan block, round 5): block 0 of the chunk pass
+// runs the scan in its table LDS before filling it, then publishes the call's
+// epoch in its descriptor's spare word (after an agent-scope release by every
+// thread); every workgroup waits for that word before it reads the scan's
+// results -- a wait on block 0 only, which is dispatched before any other, and
+// bounded by the 1 s deadline (a give-up reports on the error word).  One
+// launch per call instead of two for the small lists a bulk handle usually
+// carries.  Returns false when the wait gave up.
+__device__ __forceinline__ void fused_scan_publish(const ScanArgs &sa, uint8_t *scratch) {
+    scan_block(sa, 0, 1, scratch);
+    // every wave's stores are complete at the barrier (workgroup-scope release:
+    // s_waitcnt vmcnt(0)); one agent-scope release then publishes them all
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(sa.desc + 7, sa.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool fused_scan_wait(const ScanArgs &sa) {
+    __shared__ uint32_t ok_s;
+    if (threadIdx.x == 0) {
+        Deadline dl;
+        uint32_t ok = 1;
+        while (__hip_atomic_load(sa.desc + 7, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != sa.epoch) {
+            __builtin_amdgcn_s_sleep(2);
+            if (dl.passed()) {
+                queue_fault(14, blockIdx.x, sa.epoch);
+                ok = 0;
+                break;
+            }
+        }
+        ok_s = ok;
+    }
+    __syncthreads();
+    return ok_s != 0;
 }
 
 // (readfirstlane returns int: cast through uint32_t so nothing sign-extends)
@@ -511,19 +579,54 @@ constexpr int kSegWavesPerEU = KEY == 64 * 4 + 1 ? 8 : 1;
 
 constexpr uint64_t kSegNtBytes = 512ull << 20;
 
-template <int W, int PART>
-__global__ __launch_bounds__(1024, kSegWavesPerEU<W * 4 + PART>) void seg_kernel(SegArgs a) {
-    if (PART == 2 && *a.ragged == 0) return;  // every chunk takes the aligned pass
+// FUSED: the list fits one scan block, and block 0 scans it in this launch
+// (fused_scan_*; `sa` is read only then).  Off by default: correct (the GPU
+// segment suites pass both ways) but slower per call than the scan launch --
+// 1 x 4 KiB CRC-32C 15.8 vs 13.6 us, CRC-64 25.5 vs 20.0 us, 1024 x 4 KiB
+// CRC-64 116 vs 72 us (tools/lat_seg.py, profiles/r05/lat_seg.json): the
+// other workgroups wait on block 0's scan with an agent-scope acquire, and
+// after it the compiler can no longer keep the chunk locates' workspace loads
+// scalar.  MCHECKSUM_GPU_SEG_FUSED=1 turns it on (tests).
+#ifndef MCK_SEG_FUSED
+#define MCK_SEG_FUSED 0
+#endif
+template <int W, int PART, bool FUSED = false>
+__global__ __launch_bounds__(1024, kSegWavesPerEU<W * 4 + PART>) void seg_kernel(SegArgs a, ScanArgs sa) {
+    // the table LDS; block 0 of a fused launch scans in it before the fill
+    constexpr bool OG = W == 64 && PART == 1 && MCK_CRC64_P6;
+    __shared__ __attribute__((aligned(16))) uint8_t lds_tab[W == 32 ? kL32Bytes : OG ? kL64Main : kL64Bytes];
+    if constexpr (FUSED) {
+        // block 0 scans first (its table fill follows); the others fill their
+        // tables while it does, and wait for its epoch after the fill
+        static_assert(sizeof(lds_tab) >= kScanScratch, "scan scratch in the table LDS");
+        if (blockIdx.x == 0) fused_scan_publish(sa, lds_tab);
+    } else {
+        (void)sa;
+        if (PART == 2 && *a.ragged == 0) return;  // every chunk takes the aligned pass
+    }
     constexpr int kWPB = 1024 / 64;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWPB + (threadIdx.x >> 6));
     const uint32_t nw = gridDim.x * kWPB;
-    const uint64_t nchunks = uniform(a.C[a.nseg]);
+    uint64_t nchunks = FUSED ? 0 : uniform(a.C[a.nseg]);
     // the CRC-64 aligned chunk pass takes chunks from the work queue (the host
     // passes a slot; without one, for_each_unit strides statically)
     constexpr bool kQueue = MCK_SEG_QUEUE && (PART == 1 || PART == 3);
     __shared__ WgQueue wgq;
-    if (kQueue && threadIdx.x == 0) wg_queue_init(&wgq, a.queue, nchunks);
+    if (!FUSED && kQueue && threadIdx.x == 0) wg_queue_init(&wgq, a.queue, nchunks);
+    // after the table fill (FUSED): the scan's results, then the queue
+    auto after_fill = [&]() -> bool {
+        if constexpr (FUSED) {
+            if (!fused_scan_wait(sa)) {
+                if (threadIdx.x == 0 && a.err_word) atomicAdd(a.err_word, 1u);  // fail closed
+                return false;
+            }
+            nchunks = uniform(a.C[a.nseg]);
+            if (kQueue && threadIdx.x == 0) wg_queue_init(&wgq, a.queue, nchunks);
+            __syncthreads();
+        }
+        return true;
+    };
     // Calls body(addr, n, j, end, stop, head) for every chunk of this wave that
     // belongs to an object; true in the first wave of a launch whose queue
     // wait gave up (the caller's error word then gets +1: fail closed).
@@ -545,11 +648,12 @@ __global__ __launch_bounds__(1024, kSegWavesPerEU<W * 4 + PART>) void seg_kernel
         }
     };
     if constexpr (W == 32) {
-        __shared__ __attribute__((aligned(16))) uint8_t lds_raw[kL32Bytes];
+        uint8_t *lds_raw = lds_tab;
         const crc32_gpu_pack_t *pk = reinterpret_cast<const crc32_gpu_pack_t *>(a.pack);
         const crc32_shift_pack_t *sp = reinterpret_cast<const crc32_shift_pack_t *>(a.shift);
         fill_lds32<false, 1024>(lds_raw, pk);
         __syncthreads();
+        if (!after_fill()) return;
         const Tab32<false> lds{lds_raw};
         const uint32_t lc0 = (lane & 31u) << 2, lc1 = lc0 | 0x10000u;
         uint32_t *out = reinterpret_cast<uint32_t *>(a.out);
@@ -573,14 +677,14 @@ __global__ __launch_bounds__(1024, kSegWavesPerEU<W * 4 + PART>) void seg_kernel
         });
         if (faulted && lane == 0 && a.err_word) atomicAdd(a.err_word, 1u);
     } else {
-        // aligned chunks under the 12-lookup fold: combine operators from
-        // global memory (once per 256 KiB chunk), so two workgroups fit a CU
-        constexpr bool OG = PART == 1 && MCK_CRC64_P6;
-        __shared__ __attribute__((aligned(16))) uint8_t lds[OG ? kL64Main : kL64Bytes];
+        // aligned chunks under the 12-lookup fold (PART 1): combine operators
+        // from global memory (once per 256 KiB chunk), so two workgroups fit a CU
+        uint8_t *lds = lds_tab;
         const crc64_gpu_pack_t *pk = reinterpret_cast<const crc64_gpu_pack_t *>(a.pack);
         const crc64_shift_pack_t *sp = reinterpret_cast<const crc64_shift_pack_t *>(a.shift);
         fill_lds64<1024, OG ? kOpsGlobal : kOpsLds>(lds, pk);
         __syncthreads();
+        if (!after_fill()) return;
         const uint32_t lc = (lane & 31u) << 3;
         unsigned long long *out = reinterpret_cast<unsigned long long *>(a.out);
         // Non-temporal payload loads once the batch is far larger than the
@@ -1021,18 +1125,43 @@ int mchecksum_gpu_checksum_segments(const char *hash_method, const uint64_t *dev
     // back with the outputs below)
     const crc_rmodel_t rm = gpu_rmodel(mck_model_index(hash_method));
     const uint64_t preset = rm.rinit ^ rm.xorout;
-    uint64_t *obj_w = width == 64 && MCK_SEG_QUEUE ? (uint64_t *)a.obj : nullptr;
-    hipError_t e = launch_kernel(seg_scan, dim3((unsigned)nb), dim3(kScanThreads), s, nullptr, dev_seg_len, dev_seg_addr,
-                                 (uint64_t)nseg, desc, scan_epoch(), (uint64_t *)a.P, (uint64_t *)a.C,
-                                 (unsigned long long *)a.ragged, dev_obj_first, (uint64_t)nobj, obj_w, (uint32_t *)a.map,
-                                 a.map_cap, dev_out, (uint32_t)width, preset, a.err_word, scan_fault_block());
-    if (e != hipSuccess) return hip_err(e, "segment scan launch");
+    ScanArgs sa{};
+    sa.len = dev_seg_len;
+    sa.addr = dev_seg_addr;
+    sa.nseg = nseg;
+    sa.desc = desc;
+    sa.epoch = scan_epoch();
+    sa.P = (uint64_t *)a.P;
+    sa.C = (uint64_t *)a.C;
+    sa.ragged = (unsigned long long *)a.ragged;
+    sa.first = dev_obj_first;
+    sa.nobj = nobj;
+    sa.obj = width == 64 && MCK_SEG_QUEUE ? (uint64_t *)a.obj : nullptr;
+    sa.map = (uint32_t *)a.map;
+    sa.map_cap = a.map_cap;
+    sa.out = dev_out;
+    sa.width = (uint32_t)width;
+    sa.preset = preset;
+    sa.err_word = a.err_word;
+    sa.fault_block = scan_fault_block();
+    // A list of one scan block may be scanned by block 0 of the chunk pass
+    // itself (MCK_SEG_FUSED; MCHECKSUM_GPU_SEG_FUSED=0/1 overrides -- the tests
+    // run both).
+    const char *fenv = getenv("MCHECKSUM_GPU_SEG_FUSED");
+    const bool fused = nb == 1 && (width == 32 || MCK_SEG_MERGED) && (fenv && fenv[0] ? fenv[0] == '1' : MCK_SEG_FUSED);
+    hipError_t e = hipSuccess;
+    if (!fused) {
+        e = launch_kernel(seg_scan, dim3((unsigned)nb), dim3(kScanThreads), s, nullptr, sa);
+        if (e != hipSuccess) return hip_err(e, "segment scan launch");
+    }
     if (width == 32) {
-        e = launch_kernel(seg_kernel<32, 0>, dim3(c->cus), dim3(1024), s, nullptr, a);
+        e = fused ? launch_kernel(seg_kernel<32, 0, true>, dim3(c->cus), dim3(1024), s, nullptr, a, sa)
+                  : launch_kernel(seg_kernel<32, 0>, dim3(c->cus), dim3(1024), s, nullptr, a, sa);
     } else if (MCK_SEG_MERGED) {
         SlotRef sr = MCK_SEG_QUEUE ? queue_slot(c, stream) : SlotRef{};
         a.queue = sr.q;
-        e = launch_kernel(seg_kernel<64, 3>, dim3(c->cus), dim3(1024), s, sr.done, a);
+        e = fused ? launch_kernel(seg_kernel<64, 3, true>, dim3(c->cus), dim3(1024), s, sr.done, a, sa)
+                  : launch_kernel(seg_kernel<64, 3>, dim3(c->cus), dim3(1024), s, sr.done, a, sa);
         if (e != hipSuccess) {
             slot_unissue(c, sr);
             return hip_err(e, "segment kernel launch");
@@ -1044,11 +1173,11 @@ int mchecksum_gpu_checksum_segments(const char *hash_method, const uint64_t *dev
         // call then ends on the long aligned pass, one kernel boundary fewer
         // after it.  Only the aligned pass takes the work queue.
         a.queue = nullptr;
-        e = launch_kernel(seg_kernel<64, 2>, dim3(c->cus), dim3(1024), s, nullptr, a);
+        e = launch_kernel(seg_kernel<64, 2>, dim3(c->cus), dim3(1024), s, nullptr, a, sa);
         if (e != hipSuccess) return hip_err(e, "segment kernel launch");
         SlotRef sr = MCK_SEG_QUEUE ? queue_slot(c, stream) : SlotRef{};
         a.queue = sr.q;
-        e = launch_kernel(seg_kernel<64, 1>, dim3(2 * c->cus), dim3(1024), s, sr.done, a);
+        e = launch_kernel(seg_kernel<64, 1>, dim3(2 * c->cus), dim3(1024), s, sr.done, a, sa);
         if (e != hipSuccess) {
             slot_unissue(c, sr);
             return hip_err(e, "segment kernel launch");

@@ -397,3 +397,68 @@ def test_segment_batch_calls_on_two_streams(gpu, buf, oracle_mod):
     torch.cuda.synchronize()
     for o in outs:
         assert gpu.as_unsigned(o).tolist() == want
+
+
+# Round 5: a list of one scan block (<= 1024 segments) can be scanned inside
+# the chunk pass (MCHECKSUM_GPU_SEG_FUSED=1, mchecksum_gpu_ext.hip: block 0
+# scans, every workgroup waits for its published epoch; off by default, it
+# measured slower than the separate scan launch).  Both paths vs the oracle.
+@pytest.mark.parametrize("method", ["crc32c", "crc64", "crc64-ecma182"])
+@pytest.mark.parametrize("shape", ["one_segment", "few", "exactly_one_block", "one_past"])
+def test_segments_fused_scan_matches_scan_launch(gpu, buf, oracle_mod, method, shape, monkeypatch):
+    host = _host(buf)
+    import zlib
+    rng = np.random.default_rng(zlib.crc32(f"{method}/{shape}".encode()))
+    if shape == "one_segment":
+        segs, first = [(5, 300000)], [0, 1]
+    elif shape == "few":
+        segs, first = _objects(rng, buf.numel() - 64, 3, max_seg=3)
+    else:
+        n = 1024 if shape == "exactly_one_block" else 1025
+        lens = [int(x) for x in rng.choice([0, 1, 17, 1024, 4096, 70000], n)]
+        segs = [(int(rng.integers(0, buf.numel() - 64 - ln)), ln) for ln in lens]
+        first = sorted(set([0, n] + [int(x) for x in rng.integers(0, n, 40)]))
+    want = _want(oracle_mod, method, host, segs, first)
+    views = [buf[o:o + n] for o, n in segs]
+    monkeypatch.setenv("MCHECKSUM_GPU_SEG_FUSED", "1")
+    fused = gpu.as_unsigned(gpu.checksum_segments(method, views, first))
+    monkeypatch.setenv("MCHECKSUM_GPU_SEG_FUSED", "0")
+    launched = gpu.as_unsigned(gpu.checksum_segments(method, views, first))
+    assert fused.tolist() == want
+    assert launched.tolist() == want
+
+
+@pytest.mark.parametrize("fused", ["0", "1"])
+@pytest.mark.parametrize("method", ["crc32c", "crc64"])
+def test_segments_one_workspace_different_lists(gpu, buf, oracle_mod, method, fused, monkeypatch):
+    """One caller workspace reused by calls with different small lists, back to
+    back on one stream: every call must see its own scan (epoch-tagged; the
+    fused path's workgroups read the scan block 0 wrote in the same launch,
+    never the previous call's maps still cached)."""
+    import torch
+    from mercury_amd import _lib
+    monkeypatch.setenv("MCHECKSUM_GPU_SEG_FUSED", fused)
+    L = _lib.load_library()
+    host = _host(buf)
+    rng = np.random.default_rng(2026)
+    lists = []
+    for k in range(4):
+        segs, first = _objects(rng, buf.numel() - 64, 20 + 7 * k, max_seg=5)
+        meta = torch.from_numpy(np.concatenate([
+            np.asarray([buf.data_ptr() + o for o, _ in segs], dtype=np.uint64).view(np.int64),
+            np.asarray([n for _, n in segs], dtype=np.int64), np.asarray(first, dtype=np.int64)])).cuda()
+        lists.append((segs, first, meta, _want(oracle_mod, method, host, segs, first)))
+    nmax = max(len(s) for s, _, _, _ in lists)
+    work = torch.empty((L.mchecksum_gpu_segments_work_size(nmax) + 7) // 8, dtype=torch.int64, device="cuda")
+    outs = []
+    for rep in range(12):
+        segs, first, meta, want = lists[rep % len(lists)]
+        n, nobj, base = len(segs), len(first) - 1, meta.data_ptr()
+        out = torch.empty(nobj, dtype=torch.int64 if method == "crc64" else torch.int32, device="cuda")
+        assert L.mchecksum_gpu_checksum_segments(method.encode(), base, base + 8 * n, n, base + 16 * n, nobj,
+                                                 work.data_ptr(), work.numel() * 8, out.data_ptr(),
+                                                 torch.cuda.current_stream().cuda_stream) == 0
+        outs.append((out, want))
+    torch.cuda.synchronize()
+    for rep, (out, want) in enumerate(outs):
+        assert gpu.as_unsigned(out).tolist() == want, rep
