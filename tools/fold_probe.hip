@@ -17,7 +17,7 @@ namespace {
 constexpr int kSteps = 512;
 
 template <int CH, int MINB>
-__global__ __launch_bounds__(1024, MINB) void fold(uint64_t *sink, unsigned long long *stamps, uint64_t seed) {
+__global__ __launch_bounds__(1024, 4 * MINB) void fold(uint64_t *sink, unsigned long long *stamps, uint64_t seed) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kL64Main];
     for (uint32_t i = threadIdx.x; i < kL64Main / 8; i += 1024)
         reinterpret_cast<uint64_t *>(lds)[i] = (i + seed) * 0x9E3779B97F4A7C15ull;
@@ -42,6 +42,77 @@ __global__ __launch_bounds__(1024, MINB) void fold(uint64_t *sink, unsigned long
         stamps[2 * w] = t0;
         stamps[2 * w + 1] = t1;
     }
+}
+
+// The same fold fed by an HBM stream, as in the batch kernel's aligned loop:
+// each wave reads its own contiguous region with a 4-deep ring of 16-B
+// non-temporal loads per lane (one 1 KiB wave-load per step), 2 states per
+// lane (lo / hi 8 bytes), the data word folded in by the XOR tree.
+template <int MINB, int R>
+__global__ __launch_bounds__(1024, 4 * MINB) void stream_fold(const uint4 *data, uint64_t words_per_wave, uint64_t *sink,
+                                                           unsigned long long *stamps) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kL64Main];
+    for (uint32_t i = threadIdx.x; i < kL64Main / 8; i += 1024)
+        reinterpret_cast<uint64_t *>(lds)[i] = (i + 7) * 0x9E3779B97F4A7C15ull;
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = blockIdx.x * 16 + threadIdx.x / 64;
+    Lane64 ln = lane64((lane & 31u) << 3);
+    gbyte_t p = global_ptr(reinterpret_cast<const uint8_t *>(data + (uint64_t)wave * words_per_wave * 64 + lane), false);
+    const uint64_t K = words_per_wave;
+    uint4 ring[R];
+#pragma unroll
+    for (int u = 0; u < R; u++) ring[u] = ldg16<true>(p + u * 1024);
+    uint64_t x0 = lo64(ring[0]), x1 = hi64(ring[0]);
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    for (uint64_t k = R; k < K; k += R) {
+        p += R * 1024;
+#pragma unroll
+        for (int u = 0; u < R; u++) {
+            ring[u] = ldg16<true>(p + u * 1024);
+            const uint4 nx = ring[(u + 1) % R];
+            x0 = f64x(lds, x0, lo64(nx), ln);
+            x1 = f64x(lds, x1, hi64(nx), ln);
+        }
+    }
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    sink[blockIdx.x * 1024 + threadIdx.x] = x0 ^ x1;
+    if ((threadIdx.x & 63u) == 0) {
+        stamps[2 * wave] = t0;
+        stamps[2 * wave + 1] = t1;
+    }
+}
+
+template <int MINB, int R>
+void run_stream(int cus, const uint4 *data, uint64_t *sink, unsigned long long *stamps) {
+    const int grid = cus * MINB, waves = grid * 16;
+    const uint64_t bytes = 4ull << 30;
+    const uint64_t wpw = bytes / 1024 / waves / R * R;  // wave-steps per wave
+    std::vector<unsigned long long> h(2 * waves);
+    double best = 1e30, best_ms = 0;
+    for (int rep = 0; rep < 4; rep++) {
+        hipEvent_t e0, e1;
+        (void)hipEventCreate(&e0);
+        (void)hipEventCreate(&e1);
+        (void)hipEventRecord(e0, 0);
+        hipLaunchKernelGGL((stream_fold<MINB, R>), dim3(grid), dim3(1024), 0, 0, data, wpw, sink, stamps);
+        (void)hipEventRecord(e1, 0);
+        if (hipDeviceSynchronize() != hipSuccess) return;
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, e0, e1);
+        (void)hipMemcpy(h.data(), stamps, h.size() * 8, hipMemcpyDeviceToHost);
+        double sum = 0;
+        for (int w = 0; w < waves; w++) sum += (double)(h[2 * w + 1] - h[2 * w]);
+        const double dur = sum / waves;
+        const double cyc = dur / ((double)(waves / cus) * 2 * wpw);  // per wave-word per CU
+        if (cyc < best) {
+            best = cyc;
+            best_ms = ms;
+        }
+    }
+    const double gb = (double)waves * wpw * 1024 / 1e9;
+    printf("  HBM-fed, ring %d, %d WG/CU (%d waves/SIMD): %.1f cycles per wave-word per CU; %.3f ms for %.2f GB = %.2f TB/s\n",
+           R, MINB, 4 * MINB, best, best_ms, gb, gb / best_ms);
 }
 
 template <int CH, int MINB>
@@ -77,6 +148,15 @@ int main() {
     run<4, 1>(cus, sink, stamps);
     run<1, 2>(cus, sink, stamps);
     run<2, 2>(cus, sink, stamps);
+    uint4 *data = nullptr;
+    (void)hipMalloc(&data, (4ull << 30) + 65536);
+    (void)hipMemset(data, 0x5A, (4ull << 30) + 65536);
+    run_stream<1, 4>(cus, data, sink, stamps);
+    run_stream<1, 8>(cus, data, sink, stamps);
+    run_stream<2, 4>(cus, data, sink, stamps);
+    run_stream<1, 4>(cus, data, sink, stamps);
+    run_stream<2, 4>(cus, data, sink, stamps);
+    (void)hipFree(data);
     (void)hipFree(sink);
     (void)hipFree(stamps);
     return 0;
