@@ -35,6 +35,14 @@ if [ -z "$SKIP_NCCL" ]; then
     bench.py --gpus 1 --steps 20 --warmup 10 > $O/bench_nccl_1rank.json 2> $O/bench_nccl_1rank.err || { tail -30 $O/bench_nccl_1rank.err; exit 1; }
   cat $O/bench_nccl_1rank.json
 fi
+for c in ${TRACE_CONFIGS:-}; do
+  step "kernel trace $c (bench defaults)"
+  cd /tmp && export TMPDIR=/tmp
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$c -o bench -- python3 $R/bench.py --config $c --no-cpu-baseline > $O/prof_bench_$c.json 2> $O/prof_bench_$c.err || { tail $O/prof_bench_$c.err; exit 1; }
+  cd "$R"
+  k=crc64_batch_kernel; [ "$c" = seg ] && k=seg_kernel
+  python3 tools/trace_steady.py $O/prof_$c/bench_kernel_trace.csv $k 40 50 $O/prof_bench_$c.json > $O/${c}_kernel_steady.json && cat $O/${c}_kernel_steady.json
+done
 if [ -z "$SKIP_TRACE" ]; then
   step "kernel trace of the driver command"
   cd /tmp && export TMPDIR=/tmp
