@@ -281,8 +281,18 @@ struct ScanArgs {
     uint32_t width;
     uint64_t preset;
     uint32_t *err_word;
+    uint64_t *fault_claim;  // workspace word: the call's epoch once a fault was reported
     uint64_t fault_block;
 };
+// A call's scan-side give-ups (a look-back in any scan block, a fused chunk
+// pass's wait in any workgroup) add 1 to the error word between them, as the
+// header promises per launch: the first to swap the call's epoch into the
+// claim word reports, the rest see the epoch already there.
+__device__ __forceinline__ void report_scan_fault(const ScanArgs &sa) {
+    if (!sa.err_word) return;
+    const uint64_t was = __hip_atomic_exchange(sa.fault_claim, sa.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (was != sa.epoch) atomicAdd(sa.err_word, 1u);
+}
 // LDS scratch of one scan block: the object rows of its segments (4 x u64 +
 // u32 each) and a few broadcast words
 constexpr uint32_t kScanScratch = kScanBlk * (4 * 8 + 4) + 64;
@@ -342,7 +352,7 @@ __device__ __forceinline__ void scan_block(const ScanArgs &sa, uint64_t b, uint6
             ex[0] = ep;
             ex[1] = ec;
             ex[2] = er;
-            if (!ok && sa.err_word) atomicAdd(sa.err_word, 1u);  // fail closed: the scan is not trustworthy
+            if (!ok) report_scan_fault(sa);  // fail closed: the scan is not trustworthy
         }
     }
     __syncthreads();
@@ -618,7 +628,7 @@ __global__ __launch_bounds__(1024, kSegWavesPerEU<W * 4 + PART>) void seg_kernel
     auto after_fill = [&]() -> bool {
         if constexpr (FUSED) {
             if (!fused_scan_wait(sa)) {
-                if (threadIdx.x == 0 && a.err_word) atomicAdd(a.err_word, 1u);  // fail closed
+                if (threadIdx.x == 0) report_scan_fault(sa);  // fail closed
                 return false;
             }
             nchunks = uniform(a.C[a.nseg]);
@@ -1036,7 +1046,7 @@ using namespace mck;
 
 extern "C" {
 
-// P, C (nseg + 1 each), the ragged flag (+ pad), the look-back descriptor of
+// P, C (nseg + 1 each), the ragged flag, the scan's fault claim, the look-back descriptor of
 // each scan block (kDescWords), each segment's object and its bounds in
 // first[] and its head segment (4 nseg), then the chunk -> segment map (u32 entries:
 // 4 per segment + 64 Ki, i.e. lists averaging up to ~1 MiB per segment, or
@@ -1143,6 +1153,7 @@ int mchecksum_gpu_checksum_segments(const char *hash_method, const uint64_t *dev
     sa.width = (uint32_t)width;
     sa.preset = preset;
     sa.err_word = a.err_word;
+    sa.fault_claim = (uint64_t *)dev_work + 2 * (nseg + 1) + 1;
     sa.fault_block = scan_fault_block();
     // A list of one scan block may be scanned by block 0 of the chunk pass
     // itself (MCK_SEG_FUSED; MCHECKSUM_GPU_SEG_FUSED=0/1 overrides -- the tests

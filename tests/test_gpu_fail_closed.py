@@ -191,8 +191,8 @@ def test_segment_scan_lookback_fault(gpu, qlib, monkeypatch):
     """The one-launch segment scan's look-back in the fault-injecting build
     (MCHECKSUM_GPU_QFAULT_SCAN=1: scan block 1 gives up its wait): the call
     returns, nothing is read out of bounds (the chunk pass skips chunks whose
-    maps do not fit), and the caller's error word reports the failed scan --
-    whatever the outputs hold, they never read as verified."""
+    maps do not fit), and the caller's error word reports the failed scan once
+    -- whatever the outputs hold, they never read as verified."""
     import torch
     monkeypatch.setenv("MCHECKSUM_GPU_QFAULT_SCAN", "1")
     nseg = 3000  # three scan blocks
@@ -216,7 +216,7 @@ def test_segment_scan_lookback_fault(gpu, qlib, monkeypatch):
         qlib.mchecksum_gpu_set_error_word(None)
     assert rc == 0
     torch.cuda.synchronize()
-    assert int(word.item()) >= 1, "a scan whose look-back gave up must bump the error word"
+    assert int(word.item()) == 1, "a scan whose look-back gave up must bump the error word once"
     assert qlib.mchecksum_gpu_queue_faults() - faults0 >= 1
 
 
@@ -292,11 +292,11 @@ def test_verify_with_stalled_entry_never_reads_clean(gpu, qlib, batch, monkeypat
 
 def test_scan_descriptor_never_published_times_out(gpu, qlib, monkeypatch):
     """MCHECKSUM_GPU_QFAULT_SCAN=1 with MCHECKSUM_GPU_QFAULT_MODE=scanstall: scan
-    block 1 never publishes its look-back descriptor, so block 2 waits until
-    its deadline.  The call returns within the bound and the error word
-    reports it."""
+    block 1 never publishes its look-back descriptor, so the blocks after it
+    wait until their deadlines.  The call returns within the bound and the
+    error word reports it once, however many scan blocks gave up."""
     import torch
-    nseg = 3000  # three scan blocks
+    nseg = 6000  # six scan blocks: 2..5 may all give up
     data = torch.empty(nseg * 4096 + 64, dtype=torch.uint8, device="cuda")
     gpu.fill_splitmix(data, 0x5CA2)
     segs = [data[i * 4096:(i + 1) * 4096] for i in range(nseg)]
@@ -321,5 +321,5 @@ def test_scan_descriptor_never_published_times_out(gpu, qlib, monkeypatch):
     assert rc == [0]
     print(f"stalled scan returned after {dt:.3f} s")
     assert 0.9 <= dt <= STALL_MAX_S, f"deadline wait took {dt:.3f} s"
-    assert int(word.item()) >= 1, "a scan whose look-back timed out must bump the error word"
+    assert int(word.item()) == 1, "a scan whose look-back timed out must bump the error word once"
     assert qlib.mchecksum_gpu_queue_faults() - faults0 >= 1
