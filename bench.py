@@ -281,7 +281,11 @@ def main():
     out = torch.empty(count, dtype=G.out_dtype(method), device=dev)
     if args.streams > 1 and layout not in ("fixed", "offsets"):
         raise SystemExit(f"--streams > 1 needs a fixed or offsets layout (config {args.config} shares scratch)")
-    streams = [stream] + [torch.cuda.Stream(device=dev) for _ in range(args.streams - 1)]
+    # S > 1: S pool streams, none of them the default stream -- HIP's null
+    # stream synchronizes with the others, so a pair that includes it never
+    # overlaps (round 5: `--streams 2` with the default stream measured +-0,
+    # two pool streams +1.4%, tools/overlap_probe.py)
+    streams = [stream] if args.streams == 1 else [torch.cuda.Stream(device=dev) for _ in range(args.streams)]
     outs = [out] + [torch.empty_like(out) for _ in range(args.streams - 1)]
     torch.cuda.synchronize()
 
@@ -422,7 +426,8 @@ def report(args, r):
         "data": "synthetic (splitmix64 bytes generated on device)",
         "config": {"workload": workload, "method": r.method, "global_batch": r.global_count,
                    "payloads_rank0": r.count, "payload_bytes": r.length, "bytes_rank0": r.payload_bytes,
-                   "lanes_per_payload": r.lanes, "parallelism": f"shard{r.world}"},
+                   "lanes_per_payload": r.lanes, "parallelism": f"shard{r.world}",
+                   **({"streams": args.streams} if getattr(args, "streams", 1) > 1 else {})},
         "world_size": r.world,
         "process_group": getattr(r, "process_group", None),
         "per_rank": [dict({"rank": i, "wall_ms_per_step": round(w / args.steps * 1e3, 4), "kernel_ms": round(k, 4)},
@@ -444,6 +449,11 @@ def report(args, r):
             xdr=r.layout == "xdr")
     else:
         result["parity"] = "unchecked (--no-cpu-baseline)"
+    if getattr(args, "streams", 1) > 1:
+        # consecutive steps overlap pairwise on the GPU: kernel_ms is the event
+        # region over the steps, not one dispatch's duration (a rocprof trace
+        # shows each dispatch ~S times as long)
+        result["roofline"]["kernel_ms_is"] = f"event region / steps ({args.streams} streams overlap)"
     if r.verify_note:
         result["verify"] = r.verify_note
     return result
