@@ -21,9 +21,17 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def analyze(path):
-    rows = [r for r in csv.DictReader(open(path)) if "crc32c_batch_kernel" in r["Kernel_Name"]]
+def analyze(path, key="crc32c_batch_kernel", group=0):
+    rows = [r for r in csv.DictReader(open(path)) if key in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    if group:  # gap statistics per consecutive group of dispatches (one per probe mode)
+        for g in range(0, len(rows) - group + 1, group):
+            part = rows[g:g + group]
+            gaps = [(int(b["Start_Timestamp"]) - int(a["End_Timestamp"])) / 1e3 for a, b in zip(part, part[1:])]
+            dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in part]
+            print(json.dumps({"group": g // group, "dur_median_us": round(statistics.median(dur), 2),
+                              "gap_median_us": round(statistics.median(gaps), 2), "gap_min_us": round(min(gaps), 2)}))
+        return
     s = [int(r["Start_Timestamp"]) for r in rows]
     e = [int(r["End_Timestamp"]) for r in rows]
     gaps = [(s[i] - e[i - 1]) / 1e3 for i in range(1, len(rows))]
@@ -44,9 +52,11 @@ def main():
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--analyze")
+    ap.add_argument("--kernel", default="crc32c_batch_kernel")
+    ap.add_argument("--group", type=int, default=0)
     args = ap.parse_args()
     if args.analyze:
-        return analyze(args.analyze)
+        return analyze(args.analyze, args.kernel, args.group)
     import torch
     from mercury_amd import gpu as G
     n, length = 65536, 65536
