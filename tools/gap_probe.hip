@@ -7,6 +7,8 @@
 //   ext_stop2 the same, alternating two events
 //   ext_stop32 the same, 32 events in turn (the slot pool's pattern)
 //   rec       hipLaunchKernel, then hipEventRecord
+//   ext_nofence  ext_stop with an event made with hipEventDisableSystemFence
+//   ext_devrel   ext_stop with an event made with hipEventReleaseToDevice
 // Prints the event-timed device time per launch; run it under rocprofv3
 // --kernel-trace to read the gaps between dispatches (tools/overlap_probe.py
 // --analyze KERNEL_TRACE.csv --kernel read_nt).
@@ -53,15 +55,17 @@ int main() {
     CK(hipMalloc(&sink, 4));
     hipStream_t s;
     CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-    hipEvent_t t0, t1, ev[32];
+    hipEvent_t t0, t1, ev[32], evnf, evdr;
     CK(hipEventCreate(&t0));
     CK(hipEventCreate(&t1));
     for (int k = 0; k < 32; k++) CK(hipEventCreateWithFlags(&ev[k], hipEventDisableTiming));
+    CK(hipEventCreateWithFlags(&evnf, hipEventDisableTiming | hipEventDisableSystemFence));
+    CK(hipEventCreateWithFlags(&evdr, hipEventDisableTiming | hipEventReleaseToDevice));
     void *args[] = {&buf, (void *)&n, &sink};
-    const char *names[] = {"plain", "ext_stop", "ext_stop2", "ext_stop32", "rec"};
+    const char *names[] = {"plain", "ext_stop", "ext_stop2", "ext_stop32", "rec", "ext_nofence", "ext_devrel"};
     const int L = 20;
     for (int rep = 0; rep < 2; rep++) {
-        for (int mode = 0; mode < 5; mode++) {
+        for (int mode = 0; mode < 7; mode++) {
             for (int w = 0; w < 10; w++) hipLaunchKernelGGL(read_nt, dim3(cus), dim3(1024), 0, s, buf, n, sink);
             CK(hipEventRecord(t0, s));
             for (int i = 0; i < L; i++) {
@@ -70,7 +74,7 @@ int main() {
                     if (mode == 4) CK(hipEventRecord(ev[i & 31], s));
                 } else {
                     CK(hipExtLaunchKernel((const void *)read_nt, dim3(cus), dim3(1024), args, 0, s, nullptr,
-                                          ev[mode == 2 ? i & 1 : mode == 3 ? i & 31 : 0], 0));
+                                          mode == 5 ? evnf : mode == 6 ? evdr : ev[mode == 2 ? i & 1 : mode == 3 ? i & 31 : 0], 0));
                 }
             }
             CK(hipEventRecord(t1, s));
