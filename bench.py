@@ -282,9 +282,8 @@ def main():
     if args.streams > 1 and layout not in ("fixed", "offsets"):
         raise SystemExit(f"--streams > 1 needs a fixed or offsets layout (config {args.config} shares scratch)")
     # S > 1: S pool streams, none of them the default stream -- HIP's null
-    # stream synchronizes with the others, so a pair that includes it never
-    # overlaps (round 5: `--streams 2` with the default stream measured +-0,
-    # two pool streams +1.4%, tools/overlap_probe.py)
+    # stream is ordered against the others, so a pair that includes it never
+    # overlaps (round 5: +-0 either way without a profiler)
     streams = [stream] if args.streams == 1 else [torch.cuda.Stream(device=dev) for _ in range(args.streams)]
     outs = [out] + [torch.empty_like(out) for _ in range(args.streams - 1)]
     torch.cuda.synchronize()

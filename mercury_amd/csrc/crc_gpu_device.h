@@ -314,8 +314,32 @@ constexpr uint32_t kSplitAcc = 16;
 // (hipExtLaunchKernel's stop event, queried without blocking, queue_slot), so
 // a workgroup's exit touches no slot line.
 // Bank layout (one counter per 256-B line, 8 KiB per bank, 16 KiB-aligned
-// slots): [0, 8) sub-queue tickets, [8] fault flag of the launch -- both
-// zeroed by the previous launch on the slot.
+// slots): [0, 8) sub-queue tickets, [8] fault flag of the launch, [9, 17)
+// workgroups exited per sub-queue group, [17] groups exited -- all zeroed by
+// the previous launch on the slot; line 31 of bank 0 counts the slot's
+// completed launches (never zeroed).
+//
+// Completion without an event (late round 5, MCK_SLOT_DONE=1; off by
+// default).  Under rocprofv3 a slot launch's stop event (hipExtLaunchKernel)
+// shows ~4.3 us of idle GPU before the next dispatch on the stream, where a
+// plain launch follows its predecessor with no gap (tools/gap_probe.hip,
+// profiles/r05/gap/; also with the event's system fence disabled or a
+// device-scope release).  With MCK_SLOT_DONE=1 a slot launch reports its own
+// completion instead: each wave, after its last slot access, counts
+// itself out of its workgroup in LDS; the workgroup's last wave counts the
+// workgroup out of its sub-queue group, the group's last one counts the group
+// out of the launch, and the launch's last workgroup bumps the slot's launch
+// count and stores it to the slot's word of host-mapped memory, which the host
+// reads to reap the slot (mchecksum_gpu.hip, slot_idle).  The word is stored
+// while the launch's last waves may still finish their payloads: nothing after
+// it touches the slot.  A launch that never gets there (a fault path that
+// skips the queue) leaves its slot busy for good -- never reused, never wrong.
+// Correct (the slot, queue, thread, fail-closed, split and segment GPU suites
+// pass; tests/test_queue_model.py runs the protocol) but not faster without a
+// profiler: back-to-back series, one process, events vs completion words
+// (tools/ab_variants.py --series, profiles/r05/slot_done/): headline 0.6153 vs
+// 0.6160 ms, C4 1.2388 vs 1.2387, C3 1.3063 vs 1.3072, seg 1.3219 vs 1.3246 --
+// the gap is the profiler's.  So the stop event stays.
 //
 // Exclusivity.  A slot serves one launch at a time: the host hands the queue
 // only to eager launches, each on a slot of its stream's own (launches on one
@@ -332,11 +356,22 @@ constexpr uint32_t kSplitAcc = 16;
 constexpr uint32_t kQSub = 8;
 constexpr uint32_t kQStride = 32;  // u64 words between counters
 constexpr uint32_t kQFault = kQSub;
-constexpr uint32_t kQBankLines = kQSub + 1;  // protocol lines, zeroed before the bank's next use
+constexpr uint32_t kQExitGroup = kQSub + 1;       // + (blockIdx % kQSub)
+constexpr uint32_t kQExitTop = kQExitGroup + kQSub;
+constexpr uint32_t kQBankLines = kQExitTop + 1;  // protocol lines, zeroed before the bank's next use
+constexpr uint32_t kQLaunchLine = 31;            // bank 0 only: the slot's completed launches
 constexpr uint64_t kQBankBytes = 8192;
 constexpr uint32_t kQBankWords = (uint32_t)(kQBankBytes / 8);
 constexpr uint32_t kQSlotWords = 2 * kQBankWords;  // slots 2 * kQBankBytes aligned: bank ^ kQBankBytes = the other
-static_assert(kQBankLines * kQStride <= kQBankWords, "bank overflow");
+static_assert(kQBankLines * kQStride <= kQBankWords && kQBankLines < kQLaunchLine &&
+                  (kQLaunchLine + 1) * kQStride <= kQBankWords, "bank overflow");
+#ifndef MCK_SLOT_DONE
+#define MCK_SLOT_DONE 0
+#endif
+// The slot pool's base and the host-mapped completion words (one per slot),
+// set once per device by the host (each translation unit has its own copy).
+__device__ unsigned long long *g_mck_qbase;
+__device__ unsigned long long *g_mck_slot_done;
 // Chunk size: a power of two, about a quarter of a workgroup's fair share
 // of units, between 1 and 32 (C4: 32 units; a 5000-payload batch: 4).
 // Fixed 16 starved half the workgroups of C3's 8192 units at 2 WGs per CU; 32
@@ -420,6 +455,7 @@ constexpr uint32_t kWgRing = 8;    // LDS ring of published chunk ids
 constexpr uint64_t kNoChunk = 0xFFFFFFFFull;
 
 struct WgQueue {
+    unsigned int exits;    // waves of this workgroup done with the slot (MCK_SLOT_DONE)
     unsigned int slot;     // next (chunk, unit) slot of this workgroup
     unsigned int drained;  // sub-queues (counted from home) found empty
     unsigned int busy;     // 1: no slot for this launch -> static split
@@ -588,6 +624,7 @@ __device__ bool wg_publish(WgQueue *L, uint32_t seq, uint64_t id, uint32_t cl) {
 // front of thread 0's wave's table fill (waves look for a chunk only after
 // their first unit; until the publish they wait on the ring entry).
 __device__ __attribute__((unused)) void wg_queue_reset(WgQueue *L, unsigned long long *q) {
+    L->exits = 0;
     L->slot = 0;
     L->drained = 0;
     L->busy = q == nullptr;
@@ -610,6 +647,33 @@ __device__ __attribute__((unused)) void wg_queue_init(WgQueue *L, unsigned long 
     wg_queue_reset(L, q);
     wg_queue_start(L, q, n);
 }
+
+#if MCK_SLOT_DONE
+// 64-bit store of v at p through the vector memory path to system scope (the
+// slot's completion word in host-mapped memory)
+__device__ __forceinline__ void store_system_u64(unsigned long long *p, unsigned long long v) {
+    asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1" : : "v"(p), "v"(v) : "memory");
+}
+// A wave of a slot launch is done with the slot (see "Completion" above).
+// Every slot access before this point is an atomic (returning, or the bank
+// zeroing counted by vmcnt), so once vmcnt drains the wave's part is performed.
+__device__ __forceinline__ void slot_exit(WgQueue *L, unsigned long long *q, bool l0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (!l0) return;
+    const uint32_t waves = blockDim.x >> 6;
+    if (__hip_atomic_fetch_add(&L->exits, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP) != waves - 1) return;
+    const uint32_t g = blockIdx.x % kQSub, G = gridDim.x;
+    const unsigned long long in_group = (G - g + kQSub - 1) / kQSub, groups = G < kQSub ? G : kQSub;
+    if (atomicAdd(q + (kQExitGroup + g) * kQStride, 1ull) != in_group - 1) return;
+    if (atomicAdd(q + kQExitTop * kQStride, 1ull) != groups - 1) return;
+    // the launch's last workgroup: the slot's launch count, to the host
+    const uintptr_t slot = reinterpret_cast<uintptr_t>(q) & ~(uintptr_t)(2 * kQBankBytes - 1);
+    unsigned long long *sq = reinterpret_cast<unsigned long long *>(slot);
+    const unsigned long long n = atomicAdd(sq + kQLaunchLine * kQStride, 1ull) + 1ull;
+    const uintptr_t idx = (slot - reinterpret_cast<uintptr_t>(g_mck_qbase)) / (2 * kQBankBytes);
+    if (g_mck_slot_done) store_system_u64(g_mck_slot_done + idx, n);
+}
+#endif
 
 template <typename T>
 __device__ __forceinline__ T wave_max(T v) {
@@ -786,6 +850,9 @@ __device__ __forceinline__ bool for_each_unit(WgQueue *L, unsigned long long *qu
         uint32_t first = 0;
         if (l0 && flt) first = atomicCAS(queue + kQFault * kQStride, 0ull, 1ull) == 0ull;
         (void)nw;
+#if MCK_SLOT_DONE
+        slot_exit(L, queue, l0);
+#endif
         return __builtin_amdgcn_readfirstlane(first) != 0;
     } else {
         for (uint64_t u = FIRST ? (uint64_t)wave + nw : wave; u < n; u += nw) {

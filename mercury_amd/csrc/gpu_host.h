@@ -30,7 +30,11 @@ constexpr uint32_t kQueueSlots = kStreamSlots;
 // completion.
 struct SlotState {
     uint64_t seq = 0;            // launches enqueued on the slot: launch s counts in bank s & 1
-    hipEvent_t done = nullptr;   // recorded by the completion of the slot's latest launch (hipExtLaunchKernel stop event)
+    // MCK_SLOT_DONE: the launch itself stores the slot's completed-launch count
+    // to DevCtx::slot_done[slot] (crc_gpu_device.h, "Completion"), so the slot
+    // is idle once that word reaches seq.  Otherwise: an event recorded by the
+    // completion of the slot's latest launch (hipExtLaunchKernel stop event).
+    hipEvent_t done = nullptr;
     std::atomic<bool> pending{false};  // handed out, launch not yet enqueued (its event not yet recorded)
 };
 
@@ -51,6 +55,7 @@ struct DevCtx {
     // and take the plain static split (crc_gpu_device.h, "Exclusivity").
     unsigned long long *queue = nullptr;        // 2 * kQBankBytes-aligned view of queue_mem
     void *queue_mem = nullptr;
+    unsigned long long *slot_done = nullptr;    // host-mapped, one word per slot (MCK_SLOT_DONE)
     SlotState slot[kQueueSlots];
     uint32_t nslots = kQueueSlots;              // slots in the pool (MCHECKSUM_GPU_QUEUE_SLOTS lowers it for tests)
     std::vector<uint32_t> idle;                 // slots known idle; the most recently reaped on top (guarded by g_mu)
@@ -136,6 +141,9 @@ void slot_unissue(DevCtx *c, SlotRef &r);
 // Queue-fault count of mchecksum_gpu_ext.hip's kernels (their own copy of
 // g_mck_queue_faults) on the current device; -1 on error.
 long long ext_queue_faults();
+// Set a translation unit's copy of the slot pool base and completion words
+// (g_mck_qbase, g_mck_slot_done) on the current device.
+hipError_t ext_set_slot_globals(unsigned long long *qbase, unsigned long long *done_dev);
 // This host thread's fail-closed report word (mchecksum_gpu_set_error_word), or nullptr.
 uint32_t *error_word();
 

@@ -141,10 +141,29 @@ int device_ctx(DevCtx **out) {
         if (e == hipSuccess)
             c.queue = reinterpret_cast<unsigned long long *>((reinterpret_cast<uintptr_t>(c.queue_mem) + slot_bytes - 1) /
                                                              slot_bytes * slot_bytes);
+#if MCK_SLOT_DONE
+        // the slots' completion words: host-mapped, written by the launches
+        // (crc_gpu_device.h, "Completion"), read by slot_idle
+        unsigned long long *done_dev = nullptr;
+        if (e == hipSuccess)
+            e = hipHostMalloc(reinterpret_cast<void **>(&c.slot_done), kQueueSlots * sizeof(unsigned long long),
+                              hipHostMallocCoherent | hipHostMallocMapped);
+        if (e == hipSuccess) {
+            memset(c.slot_done, 0, kQueueSlots * sizeof(unsigned long long));
+            e = hipHostGetDevicePointer(reinterpret_cast<void **>(&done_dev), c.slot_done, 0);
+        }
+        if (e == hipSuccess)
+            e = hipMemcpyToSymbol(HIP_SYMBOL(g_mck_qbase), &c.queue, sizeof(c.queue), 0, hipMemcpyHostToDevice);
+        if (e == hipSuccess)
+            e = hipMemcpyToSymbol(HIP_SYMBOL(g_mck_slot_done), &done_dev, sizeof(done_dev), 0, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = ext_set_slot_globals(c.queue, done_dev);
+#endif
         if (e != hipSuccess) {
             if (c.queue_mem) (void)hipFree(c.queue_mem);
+            if (c.slot_done) (void)hipHostFree(c.slot_done);
             c.queue_mem = nullptr;
             c.queue = nullptr;
+            c.slot_done = nullptr;
             return hip_err(e, "work-queue allocation");
         }
         c.init = true;
@@ -190,13 +209,21 @@ int get_pack(DevCtx *c, int idx, int log2g, const void **pack) {
     return 0;
 }
 
-// Whether slot s is idle: handed to no launch that has not yet been enqueued,
-// and its latest launch has completed -- its `done` event, recorded by that
-// launch's completion (launch_kernel's stop event), queried without blocking:
-// no device round trip, so it may run under g_mu.  A never-recorded event
+// Whether slot i is idle: handed to no launch that has not yet been enqueued,
+// and its latest launch is done with it -- MCK_SLOT_DONE: the slot's
+// completed-launch count, which that launch's last workgroup stores to
+// host-mapped memory, has reached the launches enqueued on it (a plain host
+// read); otherwise its `done` event, recorded by that launch's completion
+// (launch_kernel's stop event), queried without blocking.  Neither is a
+// device round trip, so it may run under g_mu.  A never-recorded event
 // reads as complete.
-bool slot_idle(const SlotState &s) {
+bool slot_idle(const DevCtx *c, uint32_t i) {
+    const SlotState &s = c->slot[i];
     if (s.pending.load(std::memory_order_acquire)) return false;
+#if MCK_SLOT_DONE
+    // the slot's completed launches, stored by its latest launch's last workgroup
+    return __atomic_load_n(&c->slot_done[i], __ATOMIC_ACQUIRE) == s.seq;
+#endif
     const hipError_t e = hipEventQuery(s.done);
     if (e == hipSuccess) return true;
     if (e != hipErrorNotReady) (void)hipGetLastError();
@@ -237,7 +264,7 @@ SlotRef queue_slot(DevCtx *c, void *stream) {
     for (size_t k = 0; k < nlook; k++) {
         const uint32_t i = c->in_flight.front();
         c->in_flight.pop_front();
-        if (slot_idle(c->slot[i])) {
+        if (slot_idle(c, i)) {
             c->idle.push_back(i);
             c->n_reaped++;
         } else {
@@ -252,7 +279,7 @@ SlotRef queue_slot(DevCtx *c, void *stream) {
     }
     const uint32_t i = c->idle.back();
     SlotState &s = c->slot[i];
-    if (!s.done && hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess) {
+    if (!MCK_SLOT_DONE && !s.done && hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess) {
         (void)hipGetLastError();
         s.done = nullptr;
         c->n_noslot++;

@@ -1033,6 +1033,13 @@ int get_ext(DevCtx *c, int idx, const void **out) {
     return 0;
 }
 
+hipError_t ext_set_slot_globals(unsigned long long *qbase, unsigned long long *done_dev) {
+    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_mck_qbase), &qbase, sizeof(qbase), 0, hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+        e = hipMemcpyToSymbol(HIP_SYMBOL(g_mck_slot_done), &done_dev, sizeof(done_dev), 0, hipMemcpyHostToDevice);
+    return e;
+}
+
 long long ext_queue_faults() {
     unsigned int n = 0;
     if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_mck_queue_faults), sizeof(n), 0, hipMemcpyDeviceToHost) != hipSuccess)

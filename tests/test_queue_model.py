@@ -4,9 +4,17 @@ of every wave's shared-memory steps.  Checks what the GPU relies on: every
 unit is processed exactly once, no wait can block forever, and every launch
 leaves the bank the slot's next launch counts in at zero (two banks per slot,
 round 3: launch s counts in bank s & 1 and its first workgroup zeroes the
-other).  The host learns that a slot's launch has completed from the HIP event
-its completion records (round 4; queue_slot in mchecksum_gpu.hip) -- here, from
-every wave of the launch having returned.
+other).  The host learns that a slot's launch is done with the slot from the
+HIP event its completion records (round 4) or, in MCK_SLOT_DONE=1 builds
+(crc_gpu_device.h "Completion without an event"), from the slot's completion
+word -- modelled here, as the stricter of the two: every wave counts itself
+out of its workgroup, the workgroup's last wave counts the workgroup out of its
+sub-queue group, the group's last out of the launch, and the launch's last
+workgroup bumps the slot's launch count and stores it to host-mapped memory
+(crc_gpu_device.h slot_exit).  The model checks that the word is stored once
+per launch, after the launch's last access to the slot, and that a launch
+handed the slot at that moment -- while the previous one's waves still run --
+is exact.
 
 Each wave is a generator that yields at every access to shared state (LDS or
 the global slot), so a seeded scheduler explores many orders of the same
@@ -35,21 +43,24 @@ def chunk_log2(n, grid, max_log2=5):
 
 class Bank:
     def __init__(self):
-        self.sub = [0] * QSUB          # sub-queue tickets
-        self.fault = 0                 # first faulting wave of the launch
+        self.zero()
 
     def zero(self):  # wg_queue_init, workgroup 0: the protocol lines only
-        self.sub = [0] * QSUB
-        self.fault = 0
+        self.sub = [0] * QSUB          # sub-queue tickets
+        self.fault = 0                 # first faulting wave of the launch
+        self.exit_group = [0] * QSUB   # workgroups counted out, per sub-queue group
+        self.exit_top = 0              # groups counted out
 
     def clean(self):
-        return self.sub == [0] * QSUB and self.fault == 0
+        return self.sub == [0] * QSUB and self.fault == 0 and self.exit_group == [0] * QSUB and self.exit_top == 0
 
 
 class Slot:
     def __init__(self):
         self.banks = [Bank(), Bank()]
         self.issued = 0       # launches handed this slot (host: SlotState::seq)
+        self.launches = 0     # device: the slot's completed-launch line (kQLaunchLine)
+        self.done = 0         # host-mapped completion word (DevCtx::slot_done)
 
     def clean(self):
         """Ready for the next launch (the previous one has completed): the bank
@@ -59,6 +70,7 @@ class Slot:
 
 class Lds:
     def __init__(self):
+        self.exits = 0
         self.slot = 0
         self.drained = 0
         self.reads = [0] * RING
@@ -75,37 +87,52 @@ def run_model(n, grid, waves_per_wg, seed, slot=None, max_steps=2_000_000, drop=
 
 def run_launches(launches, seed, slot=None, max_steps=4_000_000):
     """Several launches, their waves interleaved at random: at most one uses the
-    slot (the host never hands one slot to two launches that can overlap); the
-    others have none (no_slot=True).  drop=(wg, seq): that workgroup's wave
-    taking slot 0 of chunk `seq` gives up (MCK_QFAULT_TEST)."""
-    assert sum(not spec.get("no_slot") for spec in launches) <= 1
+    slot at a time (the host hands a slot to a launch only once the previous
+    launch's completion word says it is done with it); the others have none
+    (no_slot=True).  after_done=True: the launch is issued on the slot at the
+    moment the previous slot launch stores its completion word -- the host's
+    reap -- while that launch's waves may still run.  drop=(wg, seq): that
+    workgroup's wave taking slot 0 of chunk `seq` gives up (MCK_QFAULT_TEST)."""
     rnd = random.Random(seed)
     slot = slot or Slot()
+    clock = [0]
     gens = []
     results = []
-    for spec in launches:
-        r = dict(units=[], slot=slot, faulted_waves=0, first_faults=0, busy_wgs=0)
+    pending = []
+
+    def issue(spec):
+        r = dict(units=[], slot=slot, faulted_waves=0, first_faults=0, busy_wgs=0, last_access=-1, done_at=[])
         results.append(r)
         bank = None
         if not spec.get("no_slot"):  # queue_slot: bank issued & 1, then count the launch
+            assert slot.done == slot.issued, "slot handed out while a launch still holds it"
             bank = (slot.banks[slot.issued & 1], slot.banks[(slot.issued & 1) ^ 1])
             slot.issued += 1
-        gens += _launch(spec, bank, rnd, r)
-    steps = 0
-    while gens:
+        gens.extend(_launch(spec, bank, rnd, r, slot, clock))
+
+    for spec in launches:
+        if spec.get("after_done"):
+            pending.append(spec)
+        else:
+            issue(spec)
+    while gens or pending:
+        if pending and slot.done == slot.issued:
+            issue(pending.pop(0))
+            continue
+        assert gens, "a launch never stored its completion word"
         g = rnd.choice(gens)
         try:
             next(g)
         except StopIteration:
             gens.remove(g)
-        steps += 1
-        assert steps < max_steps, "no progress: a wait never ends"
+        clock[0] += 1
+        assert clock[0] < max_steps, "no progress: a wait never ends"
     for r in results:
         r["units"].sort()
     return results
 
 
-def _launch(spec, bank, rnd, res):
+def _launch(spec, bank, rnd, res, slot, clock):
     n, grid, waves_per_wg, drop = spec["n"], spec["grid"], spec["wpw"], spec.get("drop")
     cl = chunk_log2(n, grid)
     cu, lead = 1 << cl, max(1, (1 << cl) // 4) if (1 << cl) > 4 else 1
@@ -126,6 +153,9 @@ def _launch(spec, bank, rnd, res):
     lds = [Lds() for _ in range(grid)]
     cur, other = bank if bank else (None, None)
 
+    def touch():  # an access to the slot's lines
+        res["last_access"] = clock[0]
+
     def fetch(L, b):  # wg_fetch
         home = b % QSUB
         d = L.drained
@@ -135,6 +165,7 @@ def _launch(spec, bank, rnd, res):
             k = home if d == 0 else (home + 1 + (d - 1 + (b // QSUB) % (QSUB - 1)) % (QSUB - 1)) % QSUB
             t = cur.sub[k]
             cur.sub[k] += 1
+            touch()
             yield
             if k + t * QSUB < nch:
                 return k + t * QSUB
@@ -194,8 +225,37 @@ def _launch(spec, bank, rnd, res):
             res["faulted_waves"] += 1
             first = cur.fault == 0  # atomicCAS(fault, 0, 1)
             cur.fault = 1
+            touch()
             yield
             res["first_faults"] += first
+        # slot_exit: this wave, its workgroup, its group, the launch
+        L.exits += 1
+        last_wave = L.exits == waves_per_wg
+        yield
+        if not last_wave:
+            return
+        g = b % QSUB
+        in_group, groups = (grid - g + QSUB - 1) // QSUB, min(grid, QSUB)
+        old = cur.exit_group[g]
+        cur.exit_group[g] += 1
+        touch()
+        yield
+        if old != in_group - 1:
+            return
+        old = cur.exit_top
+        cur.exit_top += 1
+        touch()
+        yield
+        if old != groups - 1:
+            return
+        slot.launches += 1
+        n_done = slot.launches
+        touch()
+        yield
+        slot.done = n_done  # the host-mapped word
+        res["done_at"].append(clock[0])
+        for _ in range(rnd.randint(0, 20)):  # the launch's last waves may still run
+            yield
 
     def init(b):  # wg_queue_init (thread 0 of the workgroup, before the barrier)
         L = lds[b]
@@ -205,6 +265,7 @@ def _launch(spec, bank, rnd, res):
         else:
             if b == 0:
                 other.zero()  # the slot's next launch counts there
+                touch()
                 yield
             yield from publish(L, 0, (yield from fetch(L, b)))
         yield
@@ -276,3 +337,32 @@ def test_fault_flag_is_cleared_before_its_bank_is_reused():
         assert r["units"] == list(range(900)) and r["first_faults"] == 0
         assert slot.clean()
     assert slot.banks[0].fault == 0 and slot.issued == 4
+
+
+@pytest.mark.parametrize("n,grid,wpw", [(1, 1, 1), (67, 5, 4), (1000, 9, 4), (5000, 8, 16), (20000, 12, 4),
+                                        (3000, 17, 2)])
+def test_completion_word_after_the_last_slot_access(n, grid, wpw):
+    """The launch's last workgroup stores the slot's launch count once, after
+    every access of the launch to the slot's lines (sub-queue tickets, the
+    fault flag, the exit counters, the next bank's zeroing)."""
+    slot = Slot()
+    for seed in range(3):
+        r = run_launches([dict(n=n, grid=grid, wpw=wpw)], seed * 104729 + n, slot)[0]
+        assert r["units"] == list(range(n))
+        assert len(r["done_at"]) == 1 and r["done_at"][0] > r["last_access"]
+        assert slot.done == slot.issued == seed + 1
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_next_launch_takes_the_slot_at_the_completion_word(seed):
+    """The host reaps the slot the moment the word is stored and hands it to the
+    next launch, whose waves then run beside the previous launch's last ones:
+    both hash every unit exactly once, and each stores its word once."""
+    specs = [dict(n=900, grid=6, wpw=4), dict(n=700, grid=5, wpw=4, after_done=True),
+             dict(n=1300, grid=9, wpw=2, after_done=True, drop=(1, 1)), dict(n=40, grid=3, wpw=4, after_done=True)]
+    res = run_launches(specs, seed * 7 + 3)
+    assert [r["units"] for r in res[:2]] == [list(range(900)), list(range(700))]
+    assert len(res[2]["units"]) == 1299 and res[2]["first_faults"] == 1
+    assert res[3]["units"] == list(range(40))
+    assert all(len(r["done_at"]) == 1 for r in res)
+    assert res[0]["slot"].done == res[0]["slot"].issued == 4

@@ -70,6 +70,9 @@ def main():
     ap.add_argument("--env", nargs="*", default=[],
                     help="extra pseudo-variants of the default library: NAME=VAR=VALUE (env set around its calls)")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--series", action="store_true",
+                    help="one event pair around each round's back-to-back launches (bench.py's timing: the "
+                         "boundaries between launches count) instead of one pair per launch")
     args = ap.parse_args()
 
     paths = sorted(glob.glob(os.path.join(ROOT, "build", "variants", "libmchecksum_*.so")))
@@ -126,9 +129,11 @@ def main():
                 if e:
                     os.environ[e[0]] = e[1]
                 evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                       for _ in range(args.iters)]
-                for a, b in evs:
-                    a.record(stream)
+                       for _ in range(1 if args.series else args.iters)]
+                for k in range(args.iters):
+                    a, b = evs[0 if args.series else k]
+                    if not args.series or k == 0:
+                        a.record(stream)
                     if seg is not None:
                         mb, ns = seg.meta.data_ptr(), seg.nseg
                         rc = L.mchecksum_gpu_checksum_segments(method.encode(), mb, mb + 8 * ns, ns, mb + 16 * ns, seg.nobj,
@@ -139,13 +144,14 @@ def main():
                     else:
                         rc = L.mchecksum_gpu_checksum_offsets(method.encode(), data.data_ptr(), offs.data_ptr(),
                                                               count, o.data_ptr(), h)
-                    b.record(stream)
+                    if not args.series or k == args.iters - 1:
+                        b.record(stream)
                     assert rc == 0
                 torch.cuda.synchronize()
                 if e:
                     del os.environ[e[0]]
                 if r > 0:  # round 0 = warm-up
-                    times[n] += [a.elapsed_time(b) for a, b in evs]
+                    times[n] += [a.elapsed_time(b) / (args.iters if args.series else 1) for a, b in evs]
         for n, o in zip(names, outs):
             assert torch.equal(o, ref), f"variant {n} differs from the default library"
         res = {}
