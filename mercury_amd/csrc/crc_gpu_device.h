@@ -208,9 +208,26 @@ enum OpsMode : int { kOpsLds = 0, kOpsGlobal = 1, kOpsMix = 2 };
 #ifndef MCK_CRC64_FOLD12W
 #define MCK_CRC64_FOLD12W 0
 #endif
-template <int W, int MODE, bool LIGHT = false>
+// MCK_CRC64_L8 (late round 5): aligned CRC-64 payloads at 64 lanes run with
+// ONE 64-bit state per lane -- 8 bytes per lane and step, a 512-B wave load,
+// the stride tables of the 32-lane pack (16 * 32 = 512 B) -- so the loop fits
+// 64 VGPRs and two workgroups share a CU (8 waves/SIMD, the butterflies in each
+// workgroup's LDS: 78 KiB).  tools/fold_probe.hip's steady-state series
+// promised it: the one-state loop at two workgroups per CU streamed 4 GiB in
+// 0.6433 ms against 0.6778 ms for the probe's two-state loop at one (+5.4%).
+// Built, it is bit-exact (the CRC-64 parity, split, full-shape and golden GPU
+// suites pass with it: profiles/r05/l8/) but slower than the batch kernel it
+// would replace, which already streams faster than the probe's two-state loop:
+// C3 1.3614 vs 1.3018 ms (-4.4%; ring 4: 1.3800), 64-lane payloads
+// not split 0.2141 vs 0.1820 ms (tools/ab_variants.py --series, one process).
+// Off.
+#ifndef MCK_CRC64_L8
+#define MCK_CRC64_L8 0
+#endif
+template <int W, int MODE, bool LIGHT = false, int LG = -1>
 struct Shape {
-    static constexpr bool two = W == 64 && ((MODE == 0 && !MCK_CRC64_ONE_WG) || (MODE == 2 && kCrc64OffTwo));
+    static constexpr bool l8 = W == 64 && MODE == 0 && LG == 6 && !LIGHT && MCK_CRC64_L8 && MCK_CRC64_P6;
+    static constexpr bool two = W == 64 && ((MODE == 0 && (!MCK_CRC64_ONE_WG || l8)) || (MODE == 2 && kCrc64OffTwo));
     // aligned batches at one workgroup per CU (0 = kFixedAligned): the 11-lookup
     // or the wide-row fold
     static constexpr bool one_wg_aligned = W == 64 && MODE == 0 && !two && MCK_CRC64_P6;
@@ -218,11 +235,11 @@ struct Shape {
                                 : one_wg_aligned && MCK_CRC64_FOLD12W ? kFold12W
                                                                       : kFold12;
     static constexpr bool ops_global = W == 64 && MODE == 0 && fold == kFold12 && (MCK_CRC64_SPLIT || MCK_CRC64_P6) &&
-                                       !(MCK_CRC64_ONE_WG && MCK_CRC64_ONE_WG_OPS_LDS) && !MCK_CRC64_TWO_MIX;
+                                       !(MCK_CRC64_ONE_WG && MCK_CRC64_ONE_WG_OPS_LDS) && !MCK_CRC64_TWO_MIX && !l8;
     static constexpr int block = LIGHT ? kLightBlock : two ? MCK_BLOCK64 : kBlock;
     static constexpr int blocks_per_cu = LIGHT ? 8 : two ? 2 : 1;
     static constexpr int ops_mode = ops_global ? kOpsGlobal
-                                    : fold != kFold12 || (W == 64 && MODE == 2 && kCrc64OffMix) ||
+                                    : fold != kFold12 || l8 || (W == 64 && MODE == 2 && kCrc64OffMix) ||
                                               (W == 64 && MODE == 0 && two && MCK_CRC64_TWO_MIX)
                                           ? kOpsMix
                                           : kOpsLds;
@@ -232,11 +249,12 @@ struct Shape {
                                           : ops_mode == kOpsMix       ? kL64Main + 6 * 2048
                                                                       : kL64Bytes;
 };
-// single-argument aliases (a comma inside __launch_bounds__ splits the macro)
-template <int MODE>
-constexpr int kBlk64 = Shape<64, MODE>::block;
-template <int MODE>
-constexpr int kWpe64 = Shape<64, MODE>::blocks_per_cu * Shape<64, MODE>::block / 256;
+// single-argument aliases keyed MODE * 16 + LOG2G (a comma inside
+// __launch_bounds__ splits the macro)
+template <int KEY>
+constexpr int kBlk64 = Shape<64, KEY / 16, false, KEY % 16>::block;
+template <int KEY>
+constexpr int kWpe64 = Shape<64, KEY / 16, false, KEY % 16>::blocks_per_cu * Shape<64, KEY / 16, false, KEY % 16>::block / 256;
 
 enum Mode : int { kFixedAligned = 0, kFixedGeneric = 1, kOffsets = 2 };
 
@@ -2134,6 +2152,66 @@ __device__ __forceinline__ uint64_t payload64_aligned(const uint8_t *lds, const 
     return combine64<LOG2G, OM>(lds, pk, x0, x1, gl);
 }
 
+// MCK_CRC64_L8: 64 lanes of 8 bytes per step (one state per lane; the pack
+// is the 32-lane one, whose stride tables advance 512 B), butterflies
+// Z^-(8 * 2^k) = ops[k], k = 0..5 -- the two-state loop's in-lane combine
+// (ops[0]) and its first five levels.  K steps of 512 B.
+typedef const __attribute__((address_space(1))) uint64_t *g64_t;
+template <bool NT>
+__device__ __forceinline__ uint64_t ldg8(g64_t p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+#ifndef MCK_RING64_L8
+#define MCK_RING64_L8 8
+#endif
+template <int OM>
+__device__ __forceinline__ uint64_t combine64_l8(const uint8_t *lds, const crc64_gpu_pack_t *pk, uint64_t x, uint32_t gl) {
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+        const uint64_t other = __shfl_xor(x, 1 << k, 64);
+        const bool bit = (gl >> k) & 1u;
+        const uint64_t lo = bit ? other : x, hi = bit ? x : other;
+        x = lo ^ opm64<OM>(lds, pk, k, hi);
+    }
+    return x;
+}
+template <bool NT, int OM>
+__device__ __forceinline__ uint64_t payload64_l8(const uint8_t *lds, const crc64_gpu_pack_t *pk, const uint8_t *p,
+                                                 uint32_t K, uint32_t gl, uint32_t lc, uint64_t init) {
+    constexpr int R = MCK_RING64_L8;
+    Lane64 ln = lane64(lc);
+    g64_t src = (g64_t)global_ptr(p, true) + gl;
+    uint64_t ring[R];
+    if (K % R == 0 && K >= 2 * R) {  // whole rings: no conditional load (cf. payload64_even)
+#pragma unroll
+        for (int u = 0; u < R; u++) ring[u] = ldg8<NT>(src + u * 64);
+        uint64_t x = (gl == 0 ? init : 0ull) ^ ring[0];
+        for (uint32_t k = R; k < K; k += R) {
+            src += R * 64;
+#pragma unroll
+            for (int u = 0; u < R; u++) {
+                ring[u] = ldg8<NT>(src + u * 64);
+                x = f64x(lds, x, ring[(u + 1) % R], ln);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < R; u++) x = f64x(lds, x, u + 1 < R ? ring[u + 1] : 0ull, ln);
+        return combine64_l8<OM>(lds, pk, x, gl);
+    }
+#pragma unroll
+    for (int u = 0; u < R; u++) ring[u] = (uint32_t)u < K ? ldg8<NT>(src + u * 64) : 0ull;
+    uint64_t x = (gl == 0 ? init : 0ull) ^ ring[0];
+    for (uint32_t k = 0; k < K; k += R) {
+#pragma unroll
+        for (int u = 0; u < R; u++) {
+            if (k + u + R < K) ring[u] = ldg8<NT>(src + (uint64_t)(k + u + R) * 64);
+            if (k + u < K) x = f64x(lds, x, k + u + 1 < K ? ring[(u + 1) % R] : 0ull, ln);
+        }
+    }
+    return combine64_l8<OM>(lds, pk, x, gl);
+}
+
 template <int LOG2G, bool NT, int OM = kOpsLds>
 __device__ __forceinline__ uint64_t payload64_generic(const uint8_t *lds, const crc64_gpu_pack_t *pk,
                                                       const uint8_t *p, uint64_t len, uint32_t gl, uint32_t lc) {
@@ -2269,8 +2347,8 @@ __device__ __forceinline__ uint64_t payload64_g64(const uint8_t *lds, const crc6
 // adds its term (and piece 0 the final XOR) to out[p] with a 64-bit atomic
 // XOR, into an output the host zeroed before the launch.
 template <int LOG2G, int MODE, bool VERIFY, bool NT, bool SPLIT = false>
-__global__ __launch_bounds__(kBlk64<MODE>, kWpe64<MODE>) void crc64_batch_kernel(BatchArgs a) {
-    using S = Shape<64, MODE>;
+__global__ __launch_bounds__(kBlk64<MODE * 16 + LOG2G>, kWpe64<MODE * 16 + LOG2G>) void crc64_batch_kernel(BatchArgs a) {
+    using S = Shape<64, MODE, false, LOG2G>;
     constexpr int kWPB = S::block / 64;
     __shared__ __attribute__((aligned(16))) uint8_t lds[S::lds64_bytes];
     const crc64_gpu_pack_t *pk = reinterpret_cast<const crc64_gpu_pack_t *>(a.pack);
@@ -2339,9 +2417,10 @@ __global__ __launch_bounds__(kBlk64<MODE>, kWpe64<MODE>) void crc64_batch_kernel
             for_each_unit<true, false, true>(&wgq, a.queue, units, wave, nw, [&](uint64_t u, uint32_t r) {
                 const uint64_t p = u >> sl;
                 const uint32_t q = (uint32_t)u & (pieces - 1);
-                const uint64_t x = payload64_aligned<6, NT, S::ops_mode, S::fold>(
-                    lds, pk, a.base + p * a.stride + (uint64_t)q * kSplitBytes, (uint32_t)(kSplitBytes >> 10), gl, lc,
-                    q == 0 ? pk->init : 0ull);
+                const uint8_t *src = a.base + p * a.stride + (uint64_t)q * kSplitBytes;
+                uint64_t x;
+                if constexpr (S::l8) x = payload64_l8<NT, S::ops_mode>(lds, pk, src, (uint32_t)(kSplitBytes >> 9), gl, lc, q == 0 ? pk->init : 0ull);
+                else x = payload64_aligned<6, NT, S::ops_mode, S::fold>(lds, pk, src, (uint32_t)(kSplitBytes >> 10), gl, lc, q == 0 ? pk->init : 0ull);
                 if (gl == 0) {
                     const uint64_t t = shift64(sp, x, (uint64_t)(pieces - 1 - q) * kSplitBytes) ^ (q == 0 ? xorout : 0ull);
                     if (in_wg) {
@@ -2367,7 +2446,9 @@ __global__ __launch_bounds__(kBlk64<MODE>, kWpe64<MODE>) void crc64_batch_kernel
         const bool act = p < a.count;
         const uint64_t pc = act ? p : a.count - 1;
         uint64_t x;
-        if constexpr (MODE == kFixedAligned)
+        if constexpr (S::l8)
+            x = payload64_l8<NT, S::ops_mode>(lds, pk, a.base + pc * a.stride, (uint32_t)(a.len >> 9), gl, lc, pk->init);
+        else if constexpr (MODE == kFixedAligned)
             x = payload64_aligned<LOG2G, NT, S::ops_mode, S::fold>(lds, pk, a.base + pc * a.stride, (uint32_t)(a.len >> (4 + LOG2G)), gl, lc, pk->init);
         else
             x = payload64_generic<LOG2G, NT>(lds, pk, a.base + pc * a.stride, a.len, gl, lc);

@@ -379,7 +379,7 @@ int choose_log2g(size_t len, int width) {
 
 template <int W, int LOG2G, int MODE, bool VERIFY, bool NT = false, bool LIGHT = false>
 KLaunch kernel_ptr() {
-    using S = Shape<W, MODE, LIGHT>;
+    using S = Shape<W, MODE, LIGHT, LOG2G>;
     if constexpr (W == 32) return {crc32c_batch_kernel<LOG2G, MODE, VERIFY, NT, LIGHT>, S::block, S::blocks_per_cu};
     else return {crc64_batch_kernel<LOG2G, MODE, VERIFY, NT>, S::block, S::blocks_per_cu};
 }
@@ -568,6 +568,13 @@ int launch_fixed(DevCtx *c, int idx, const void *pack, int width, int lg, const 
     // load ring depth; everything else takes the generic path.
     const bool aligned = ((uintptr_t)dev_base % 16 == 0) && (stride % 16 == 0 || count == 1) &&
                          len >= step * kRing && (len % (step * kRing) == 0) && (len >> (4 + lg)) < (1ull << 31) && !getenv("MCHECKSUM_GPU_FORCE_GENERIC");
+    // the one-state CRC-64 loop at 64 lanes (MCK_CRC64_L8) steps 512 B: the
+    // 32-lane pack's stride tables
+    if (Shape<64, kFixedAligned, false, 6>::l8 && width == 64 && lg == 6 && aligned && !light) {
+        std::lock_guard<std::mutex> lk(g_mu);
+        const int rc = get_pack(c, idx, 5, &pack);
+        if (rc) return rc;
+    }
     BatchArgs a{};
     a.base = (const uint8_t *)dev_base;
     a.stride = stride;
@@ -588,10 +595,9 @@ int launch_fixed(DevCtx *c, int idx, const void *pack, int width, int lg, const 
         }
         a.shift = shift;
         a.split_log2 = sl;
-        const KLaunch k = nt ? KLaunch{crc64_batch_kernel<6, kFixedAligned, false, true, true>, Shape<64, kFixedAligned>::block,
-                                       Shape<64, kFixedAligned>::blocks_per_cu}
-                             : KLaunch{crc64_batch_kernel<6, kFixedAligned, false, false, true>, Shape<64, kFixedAligned>::block,
-                                       Shape<64, kFixedAligned>::blocks_per_cu};
+        using S6 = Shape<64, kFixedAligned, false, 6>;
+        const KLaunch k = nt ? KLaunch{crc64_batch_kernel<6, kFixedAligned, false, true, true>, S6::block, S6::blocks_per_cu}
+                             : KLaunch{crc64_batch_kernel<6, kFixedAligned, false, false, true>, S6::block, S6::blocks_per_cu};
         const unsigned grid = grid_for(c, (uint64_t)count << sl, k);
         SlotRef sr = queue_slot(c, stream);
         a.queue = sr.q;

@@ -33,6 +33,7 @@ SHAPES = {
     "g16k": ("crc64", 32768, 16384, 0x4D43310000000003),
     "g64k": ("crc64", 16384, 65536, 0x4D43310000000003),
     "c3": ("crc64", 8192, 1 << 20, 0x4D43310000000003),
+    "m1": ("crc64", 256, 1 << 20, 0x4D43310000000003),     # 256 MiB: 64-lane CRC-64 payloads, not split
     "c4": ("crc32c", 262144, None, 0x4D43310000000004),   # offsets table, U[64 B, 64 KiB]
     "c4_64": ("crc64", 262144, None, 0x4D43310000000004),
     "seg": ("crc64", 8192, "seg", 0x4D43310000000003),      # bench.py's segments layout
