@@ -283,7 +283,7 @@ struct BatchArgs {
     // MSB-first model on a verify call: the kernel's value is the CRC
     // byte-swapped (crc_gpu_layout.h), so swap before comparing
     uint32_t bswap;
-    // split CRC-64: 1 = every queue chunk holds whole payloads (split_chunks_whole),
+    // split CRC-64: 1 = every queue chunk holds whole payloads (SplitPlan::whole),
     // so the pieces combine in the workgroup's LDS and out[] needs no zeroing
     uint32_t split_lds;
 };
@@ -459,16 +459,66 @@ struct ChunkPlan {
     }
     __device__ __forceinline__ uint32_t size(uint64_t id) const { return id < nbig ? 1u << cl : 1u << sl; }
 };
-// Split CRC-64: does every queue chunk of `units` pieces (`pieces` per payload,
-// a power of two) on `grid` workgroups hold whole payloads, at most kSplitAcc
-// of them?  (ChunkPlan's sizes; chunk starts are multiples of the tail size.)
-__host__ __device__ inline bool split_chunks_whole(uint64_t units, uint32_t grid, uint32_t pieces) {
-    const uint64_t share = units / (4ull * grid);
-    uint32_t cl = 0;
-    while (cl < kWgChunkMaxLog2 && (2ull << cl) <= share) cl++;
-    const uint32_t sl = MCK_QTAIL && cl >= MCK_QTAIL_SHIFT ? cl - MCK_QTAIL_SHIFT : cl;
-    return pieces >= 2 && pieces <= (1u << sl) && (1u << cl) / pieces <= kSplitAcc;
-}
+// Split CRC-64 (late round 5): the queue plan of a split launch.  The bulk is
+// ChunkPlan's full chunks of whole payloads in kSplitBytes pieces.  With
+// MCK_SPLIT_TAIL = t > 0 the tail -- ChunkPlan's last full chunk per
+// workgroup -- goes out one payload per chunk in 2^t times smaller pieces
+// (2^tsl = 2^t * 2^psl units), so a workgroup's waves share a tail payload.
+// C3's per-wave trace motivated it (tools/tail_trace.py,
+// profiles/r05/split_tail/): 146 us per 256 KiB piece, waves ending 1166 (p10)
+// to 1278 us (max), ~5.6% of the waves' time idle in the end game, against an
+// 18 us spread on the headline's 37 us units.  With quarter pieces the spread
+// fell to 42 us (1224..1266 us) -- but every piece pays its own combine and
+// Z^n shift, and the waves' busy time grew by as much: C3 1.3161 (quarter) /
+// 1.3186 (half) vs 1.3101 ms (ChunkPlan), one process, 10 rounds.  Off (0):
+// ChunkPlan's layout exactly.  Only when a payload's finer pieces fit one
+// chunk (psl + t <= cl).
+#ifndef MCK_SPLIT_TAIL
+#define MCK_SPLIT_TAIL 0  // log2 of how much finer the tail pieces are
+#endif
+struct SplitPlan {
+    uint32_t cl, sl;       // log2 of the full / tail chunk size (units)
+    uint32_t psl, tsl;     // log2 pieces per bulk / tail payload
+    uint64_t nbig, nch, big_end, n, bpay;
+    __host__ __device__ SplitPlan(uint64_t count, uint32_t psl_, uint32_t grid) : psl(psl_) {
+        const uint64_t n0 = count << psl;
+        const uint64_t share = n0 / (4ull * grid);
+        cl = 0;
+        while (cl < kWgChunkMaxLog2 && (2ull << cl) <= share) cl++;
+        const bool refine = MCK_SPLIT_TAIL && psl + MCK_SPLIT_TAIL <= cl;
+        tsl = refine ? psl + MCK_SPLIT_TAIL : psl;
+        sl = refine ? tsl : (MCK_QTAIL && cl >= MCK_QTAIL_SHIFT ? cl - MCK_QTAIL_SHIFT : cl);
+        const uint64_t tail = (uint64_t)MCK_QTAIL_CHUNKS * grid << cl;
+        nbig = n0 > tail ? (n0 - tail) >> cl : 0;
+        big_end = nbig << cl;
+        bpay = big_end >> psl;  // whole payloads (cl >= psl whenever refine)
+        n = refine ? big_end + ((count - bpay) << tsl) : n0;
+        nch = nbig + ((n - big_end + (1ull << sl) - 1) >> sl);
+    }
+    __host__ __device__ uint64_t start(uint64_t id) const { return id < nbig ? id << cl : big_end + ((id - nbig) << sl); }
+    __host__ __device__ uint32_t size(uint64_t id) const { return id < nbig ? 1u << cl : 1u << sl; }
+    // unit u: payload *p, piece *q of 2^*lg pieces
+    __host__ __device__ void unit(uint64_t u, uint64_t *p, uint32_t *q, uint32_t *lg) const {
+        if (u < big_end || tsl == psl) {
+            *p = u >> psl;
+            *q = (uint32_t)u & ((1u << psl) - 1u);
+            *lg = psl;
+        } else {
+            const uint64_t v = u - big_end;
+            *p = bpay + (v >> tsl);
+            *q = (uint32_t)v & ((1u << tsl) - 1u);
+            *lg = tsl;
+        }
+    }
+    // every chunk holds whole payloads, at most kSplitAcc of them (the
+    // in-workgroup combine, split_lds)
+    __host__ __device__ bool whole() const {
+        if (psl < 1) return false;
+        if (tsl != psl) return cl >= psl && (1u << (cl - psl)) <= kSplitAcc;
+        return (1u << psl) <= (1u << sl) && (1u << cl) / (1u << psl) <= kSplitAcc;
+    }
+};
+
 constexpr uint32_t kWgRing = 8;    // LDS ring of published chunk ids
 constexpr uint64_t kNoChunk = 0xFFFFFFFFull;
 
@@ -651,19 +701,28 @@ __device__ __attribute__((unused)) void wg_queue_reset(WgQueue *L, unsigned long
         L->entry[r] = ~0ull;
     }
 }
-__device__ __attribute__((unused)) void wg_queue_start(WgQueue *L, unsigned long long *q, uint64_t n) {
+template <class Plan>
+__device__ __attribute__((unused)) void wg_queue_start_plan(WgQueue *L, unsigned long long *q, const Plan &plan) {
     if (!q) return;
     if (blockIdx.x == 0) {
         unsigned long long *o = reinterpret_cast<unsigned long long *>(reinterpret_cast<uintptr_t>(q) ^ kQBankBytes);
 #pragma unroll
         for (uint32_t j = 0; j < kQBankLines; j++) atomicExch(o + j * kQStride, 0ull);
     }
-    const ChunkPlan plan(n);
     (void)wg_publish(L, 0, wg_fetch(L, q, plan.nch), plan.cl);
+}
+__device__ __attribute__((unused)) void wg_queue_start(WgQueue *L, unsigned long long *q, uint64_t n) {
+    if (!q) return;
+    wg_queue_start_plan(L, q, ChunkPlan(n));
 }
 __device__ __attribute__((unused)) void wg_queue_init(WgQueue *L, unsigned long long *q, uint64_t n) {
     wg_queue_reset(L, q);
     wg_queue_start(L, q, n);
+}
+template <class Plan>
+__device__ __attribute__((unused)) void wg_queue_init_plan(WgQueue *L, unsigned long long *q, const Plan &plan) {
+    wg_queue_reset(L, q);
+    wg_queue_start_plan(L, q, plan);
 }
 
 #if MCK_SLOT_DONE
@@ -727,9 +786,9 @@ __device__ __forceinline__ uint64_t first_static_units(uint64_t n, uint32_t nw) 
 // its chunk's ring entry r, and a taker counts itself a reader of the entry
 // only once body has returned -- the entry is not republished while any of
 // its units runs, so per-entry state in LDS outlives them all.
-template <bool DYN, bool FIRST = false, bool DEFER = false, class F>
+template <bool DYN, bool FIRST = false, bool DEFER = false, class Plan = ChunkPlan, class F>
 __device__ __forceinline__ bool for_each_unit(WgQueue *L, unsigned long long *queue, uint64_t n, uint32_t wave,
-                                              uint32_t nw, F &&body) {
+                                              uint32_t nw, F &&body, const Plan *given = nullptr) {
     if constexpr (DYN) {
         // One call site of body for both splits: a second inlined copy of the
         // payload loop made the offsets kernels spill, and so does the copy
@@ -741,7 +800,10 @@ __device__ __forceinline__ bool for_each_unit(WgQueue *L, unsigned long long *qu
 #ifndef MCK_QLEAD_DIV
 #define MCK_QLEAD_DIV 4
 #endif
-        const ChunkPlan plan(n - q0);
+        const Plan plan = [&] {
+            if constexpr (std::is_same_v<Plan, ChunkPlan>) return given ? *given : ChunkPlan(n - q0);
+            else return *given;
+        }();
         const uint32_t cl = plan.cl, cu = 1u << cl, lead = cu > MCK_QLEAD_DIV ? cu / MCK_QLEAD_DIV : 1;
         const uint64_t nch = plan.nch;
 #if MCK_TRACE
@@ -2353,11 +2415,16 @@ __global__ __launch_bounds__(kBlk64<MODE * 16 + LOG2G>, kWpe64<MODE * 16 + LOG2G
     __shared__ __attribute__((aligned(16))) uint8_t lds[S::lds64_bytes];
     const crc64_gpu_pack_t *pk = reinterpret_cast<const crc64_gpu_pack_t *>(a.pack);
     constexpr int PPW = 64 >> LOG2G;
-    const uint64_t units = MODE == kOffsets ? a.count : SPLIT ? a.count << a.split_log2 : (a.count + PPW - 1) / PPW;
+    // split launches: the plan with the finer tail pieces (SplitPlan)
+    const SplitPlan splan(SPLIT ? a.count : 0, SPLIT ? a.split_log2 : 1u, gridDim.x);
+    const uint64_t units = MODE == kOffsets ? a.count : SPLIT ? splan.n : (a.count + PPW - 1) / PPW;
     __shared__ WgQueue wgq;
     constexpr bool DYN = dyn_policy(64, MODE, NT, false) || SPLIT;
     MCK_STAMP(blockIdx.x * kWPB + (threadIdx.x >> 6), 0);
-    if (DYN && threadIdx.x == 0) wg_queue_init(&wgq, a.queue, units);
+    if (DYN && threadIdx.x == 0) {
+        if constexpr (SPLIT) wg_queue_init_plan(&wgq, a.queue, splan);
+        else wg_queue_init(&wgq, a.queue, units);
+    }
     // split pieces combined in the workgroup (SPLIT, split_lds)
     __shared__ unsigned long long sacc[SPLIT ? kWgRing * kSplitAcc : 1];
     __shared__ unsigned int scnt[SPLIT ? kWgRing * kSplitAcc : 1];
@@ -2395,7 +2462,6 @@ __global__ __launch_bounds__(kBlk64<MODE * 16 + LOG2G>, kWpe64<MODE * 16 + LOG2G
     }
     if constexpr (SPLIT) {
         static_assert(LOG2G == 6 && MODE == kFixedAligned && !VERIFY, "split pieces: aligned G = 64 checksums");
-        const uint32_t sl = a.split_log2, pieces = 1u << sl;
         const crc64_shift_pack_t *sp = reinterpret_cast<const crc64_shift_pack_t *>(a.shift);
         unsigned long long *out = reinterpret_cast<unsigned long long *>(a.out);
         // In-workgroup combine (split_lds, a slot launch whose queue chunks hold
@@ -2405,24 +2471,27 @@ __global__ __launch_bounds__(kBlk64<MODE * 16 + LOG2G>, kWpe64<MODE * 16 + LOG2G
         // split) each piece XORs its term into the out[] the host zeroed.
         // (The host's check is repeated here: a mismatch is a fault, never a
         // silently wrong value.)
-        const bool in_wg = a.split_lds && a.queue && split_chunks_whole(units, gridDim.x, pieces);
+        const bool in_wg = a.split_lds && a.queue && splan.whole();
         if (a.split_lds && !in_wg) {  // host and device disagree: fail closed, reported once per launch
             if (blockIdx.x == 0 && threadIdx.x < 64) {
-                if (threadIdx.x == 0) queue_fault(13, units, pieces);
+                if (threadIdx.x == 0) queue_fault(13, units, a.split_log2);
                 fail_closed<false>(a);
             }
             return;
         }
         const bool faulted =
-            for_each_unit<true, false, true>(&wgq, a.queue, units, wave, nw, [&](uint64_t u, uint32_t r) {
-                const uint64_t p = u >> sl;
-                const uint32_t q = (uint32_t)u & (pieces - 1);
-                const uint8_t *src = a.base + p * a.stride + (uint64_t)q * kSplitBytes;
+            for_each_unit<true, false, true, SplitPlan>(&wgq, a.queue, units, wave, nw, [&](uint64_t u, uint32_t r) {
+                uint64_t p;
+                uint32_t q, lg;
+                splan.unit(u, &p, &q, &lg);
+                const uint32_t pieces = 1u << lg;
+                const uint64_t bytes = a.len >> lg;  // this payload's piece size (kSplitBytes, or a quarter in the tail)
+                const uint8_t *src = a.base + p * a.stride + (uint64_t)q * bytes;
                 uint64_t x;
-                if constexpr (S::l8) x = payload64_l8<NT, S::ops_mode>(lds, pk, src, (uint32_t)(kSplitBytes >> 9), gl, lc, q == 0 ? pk->init : 0ull);
-                else x = payload64_aligned<6, NT, S::ops_mode, S::fold>(lds, pk, src, (uint32_t)(kSplitBytes >> 10), gl, lc, q == 0 ? pk->init : 0ull);
+                if constexpr (S::l8) x = payload64_l8<NT, S::ops_mode>(lds, pk, src, (uint32_t)(bytes >> 9), gl, lc, q == 0 ? pk->init : 0ull);
+                else x = payload64_aligned<6, NT, S::ops_mode, S::fold>(lds, pk, src, (uint32_t)(bytes >> 10), gl, lc, q == 0 ? pk->init : 0ull);
                 if (gl == 0) {
-                    const uint64_t t = shift64(sp, x, (uint64_t)(pieces - 1 - q) * kSplitBytes) ^ (q == 0 ? xorout : 0ull);
+                    const uint64_t t = shift64(sp, x, (uint64_t)(pieces - 1 - q) * bytes) ^ (q == 0 ? xorout : 0ull);
                     if (in_wg) {
                         // (one wave's LDS atomics are performed in order: a piece's
                         // XOR lands before its count)
@@ -2437,8 +2506,9 @@ __global__ __launch_bounds__(kBlk64<MODE * 16 + LOG2G>, kWpe64<MODE * 16 + LOG2G
                         atomicXor(out + p, (unsigned long long)t);
                     }
                 }
-            });
+            }, &splan);
         if (faulted) fail_closed<false>(a);
+        MCK_STAMP(blockIdx.x * kWPB + (threadIdx.x >> 6), 2);
         return;
     }
     const bool faulted = for_each_unit<DYN>(&wgq, a.queue, units, wave, nw, [&](uint64_t u) {

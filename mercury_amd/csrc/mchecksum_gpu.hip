@@ -586,7 +586,8 @@ int launch_fixed(DevCtx *c, int idx, const void *pack, int width, int lg, const 
     const bool nt = !light && use_nt((uint64_t)len * count);
     uint32_t sl = 0;
     while ((kSplitBytes << sl) < len && sl < 63) sl++;
-    if (use_split(width, lg, aligned, nt, len, count > 1 ? stride : 16) && ((uint64_t)count << sl) <= kMaxUnits) {
+    // (the split plan's tail pieces are a quarter size: up to 4x the units)
+    if (use_split(width, lg, aligned, nt, len, count > 1 ? stride : 16) && ((uint64_t)count << (sl + 2)) <= kMaxUnits) {
         const void *shift = nullptr;
         {
             std::lock_guard<std::mutex> lk(g_mu);
@@ -607,7 +608,7 @@ int launch_fixed(DevCtx *c, int idx, const void *pack, int width, int lg, const 
         // -- a hipMemsetAsync captured into a graph did not order against the
         // kernel node on replays after the first (the pieces landed in a
         // half-zeroed output: tests/test_gpu_queue.py, concurrent replays).
-        a.split_lds = sr.q && use_split_lds() && split_chunks_whole((uint64_t)count << sl, grid, 1u << sl) ? 1u : 0u;
+        a.split_lds = sr.q && use_split_lds() && SplitPlan(count, sl, grid).whole() ? 1u : 0u;
         if (!a.split_lds) {
             uint64_t zb = (count + 255) / 256;
             zb = zb > 1024 ? 1024 : zb;

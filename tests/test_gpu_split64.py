@@ -1,6 +1,6 @@
 """Split CRC-64 (crc_gpu_device.h, crc64_batch_kernel<..., SPLIT>): large
 aligned payloads run as 256 KiB pieces on the work queue.  When every queue
-chunk holds whole payloads (split_chunks_whole) the pieces combine in their
+chunk holds whole payloads (SplitPlan::whole) the pieces combine in their
 workgroup's LDS and the last one stores the CRC; otherwise -- graph captures,
 plans whose chunks cut payloads -- they XOR into an output zeroed by a kernel
 first.  Both ways against the oracle (MCHECKSUM_GPU_SPLIT_LDS=0 forces the
