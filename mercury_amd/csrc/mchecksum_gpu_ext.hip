@@ -101,7 +101,12 @@ struct SegArgs {
 // launch presets out[j] = init ^ xorout.  Round 3 ran this as a block-reduce
 // launch and a block-offset launch (4.8 + 8.5 us at 32768 segments, beside a
 // kernel boundary), round 2 as three.
-constexpr uint32_t kScanThreads = 256, kScanPer = 4, kScanBlk = kScanThreads * kScanPer;
+// (MCK_SCAN_PER 1 / 2 -- 4x / 2x the scan blocks -- measured +-0.1% on the
+// bench's 32768-segment lists, profiles/r05/scan_per/)
+#ifndef MCK_SCAN_PER
+#define MCK_SCAN_PER 4  // segments per scan thread
+#endif
+constexpr uint32_t kScanThreads = 256, kScanPer = MCK_SCAN_PER, kScanBlk = kScanThreads * kScanPer;
 constexpr uint32_t kDescWords = 8;  // per scan block: flag, aggregate (p, c, r), inclusive (p, c, r), pad
 
 __device__ __forceinline__ uint64_t seg_chunks(uint64_t l) { return (l + kChunk - 1) / kChunk; }
