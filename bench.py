@@ -89,6 +89,13 @@ def parse():
                    help="nccl = RCCL (default); gloo only to rehearse the multi-rank flow on one GPU")
     p.add_argument("--no-c5-strong", action="store_true",
                    help="skip the c5_strong sub-record of the default (headline) run")
+    p.add_argument("--no-e2e", action="store_true",
+                   help="skip the e2e sub-record of the default (headline) run at N=1 (host memory -> GPU -> host)")
+    p.add_argument("--e2e-reps", type=int, default=5, help="timed passes per e2e leg (median reported)")
+    p.add_argument("--rotate", type=int, default=None,
+                   help="fixed layouts: step i reads batch i %% R of R equal batches at distinct addresses, so no "
+                        "launch re-reads what the previous one left in the 256 MiB Infinity Cache "
+                        "(default: 4 for c2, whose 256 MiB batch fits that cache; 1 otherwise)")
     return p.parse_args()
 
 
@@ -187,6 +194,12 @@ def main():
         # scaling).  Measured first, so the headline's dispatches are the last
         # of their kernel in a profile of this command.
         c5_strong = run_c5_strong(args, torch, dist, dist_on, rank, world, dev, coll_dev)
+    e2e = None
+    if args.config == "metric" and not args.no_e2e and world == 1:
+        # north_star's end-to-end rate: the headline's bytes starting and
+        # ending in host memory (NA recv buffers / hg_proc buffers).  Before
+        # the headline, so its dispatches stay the last of their kernel.
+        e2e = run_e2e(args, torch, dev)
 
     from mercury_amd import gpu as G
     from mercury_amd.shard import batch_shard
@@ -209,13 +222,21 @@ def main():
     stream = torch.cuda.current_stream()
     G.prepare(method)
 
+    rotate = args.rotate if args.rotate is not None else (4 if args.config == "c2" else 1)
+    if rotate < 1 or (rotate > 1 and layout != "fixed"):
+        raise SystemExit("--rotate needs R >= 1, and R > 1 a fixed layout")
+    datas = None
     # ---- this rank's share of the global batch, generated on the device ----
     if layout == "fixed":
-        data = torch.empty(plan.nbytes + 64, dtype=torch.uint8, device=dev)
-        G.fill_splitmix(data, seed, first_word=plan.first_word)  # the global stream's bytes
+        # R copies of the share at distinct addresses (R > 1: every launch
+        # reads cold lines -- the previous launch read another copy)
+        datas = [torch.empty(plan.nbytes + 64, dtype=torch.uint8, device=dev) for _ in range(rotate)]
+        for d in datas:
+            G.fill_splitmix(d, seed, first_word=plan.first_word)  # the global stream's bytes
+        data = datas[0]
         offsets_dev = offsets_host = None
         payload_bytes = plan.nbytes
-        run = lambda out: G.checksum_fixed(method, data, length, count=count, out=out)  # noqa: E731
+        run = lambda out, b=0: G.checksum_fixed(method, datas[b], length, count=count, out=out)  # noqa: E731
     elif layout == "segments":  # per-rank objects (weak): scattered segment lists
         from mercury_amd.workload import segment_slots
         seg_len = length // SEGS_PER_OBJECT
@@ -288,10 +309,13 @@ def main():
     outs = [out] + [torch.empty_like(out) for _ in range(args.streams - 1)]
     torch.cuda.synchronize()
 
-    def step(i):  # step i: one batch, on stream i % S with its own output
+    def step(i):  # step i: one batch (copy i % R), on stream i % S with its own output
         s = streams[i % len(streams)]
         with torch.cuda.stream(s):
-            run(outs[i % len(streams)])
+            if rotate > 1:
+                run(outs[i % len(streams)], i % rotate)
+            else:
+                run(outs[i % len(streams)])
         return s
 
     for i in range(args.warmup):
@@ -323,6 +347,30 @@ def main():
         dist.barrier()
     wall = time.perf_counter() - t0
     kern_ms = ev_start.elapsed_time(ev_end) / args.steps
+
+    rotation = None
+    if rotate > 1:
+        # every copy gives the same CRCs, and the replay figure of copy 0 alone
+        # (each launch re-reads what the last one left in the Infinity Cache),
+        # kept only as a labelled cache-warm number
+        outs_r = [torch.empty_like(out) for _ in range(rotate)]
+        for b in range(rotate):
+            run(outs_r[b], b)
+        same = all(torch.equal(outs_r[0], o) for o in outs_r[1:])
+        for _ in range(args.warmup):
+            run(out, 0)
+        ew0, ew1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        ew0.record()
+        for _ in range(args.steps):
+            run(out, 0)
+        ew1.record()
+        torch.cuda.synchronize()
+        warm_ms = ew0.elapsed_time(ew1) / args.steps
+        rotation = {"copies": rotate, "bytes_per_copy": payload_bytes, "copies_agree": same,
+                    "cache_warm": {"kernel_ms": round(warm_ms, 4),
+                                   "GiB_s": round(payload_bytes / (warm_ms * 1e-3) / 2**30, 2),
+                                   "note": "replay of ONE copy back to back (Infinity-Cache warm; not HBM evidence)"}}
 
     t = torch.tensor([wall, kern_ms], dtype=torch.float64, device=coll_dev)
     per_rank = [t.clone() for _ in range(world)]
@@ -387,6 +435,12 @@ def main():
             c5_strong.pop("_got", None)
             c5_strong.pop("_firsts", None)
             result["c5_strong"] = c5_strong
+        if rotation is not None:
+            result["rotation"] = rotation
+            result["roofline"]["cache"] = (f"cold: step i reads copy i % {rotate} of {rotate} at distinct addresses "
+                                           f"({rotate * payload_bytes / 2**20:.0f} MiB in all)")
+        if e2e is not None:
+            result["e2e"] = e2e_finish(e2e, got, args)
         print(json.dumps(result), flush=True)
     if dist_on:
         dist.barrier()
@@ -536,6 +590,196 @@ def run_c5_strong(args, torch, dist, dist_on, rank, world, dev, coll_dev):
         "_got": got,
         "_firsts": share_firsts(plan, "fixed", world, plan.count),
     }
+
+
+PCIE_GEN5_X16_GBS = 63.0  # 32 GT/s x 16 lanes, 128b/130b encoding, per direction
+
+
+def _hip():
+    """libamdhip64 (the one torch loaded) for the host-memory calls torch does not wrap."""
+    import ctypes
+    import torch
+    lib = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so"))
+    vp = ctypes.c_void_p
+    lib.hipHostGetDevicePointer.argtypes = [ctypes.POINTER(vp), vp, ctypes.c_uint]
+    lib.hipHostGetDevicePointer.restype = ctypes.c_int
+    return lib
+
+
+def run_e2e(args, torch, dev):
+    """The e2e sub-record of the default run (N = 1): the headline's 65536 x
+    64 KiB payloads starting and ending in HOST memory, as Mercury's NA recv
+    buffers and hg_proc buffers are (src/mercury_core.c:4667-4714 hands the
+    received bytes to the proc layer).  Three legs over the same pinned 4 GiB,
+    each the median of --e2e-reps timed passes after one untimed pass:
+
+      staged    -- H2D in 128 MiB chunks on a copy stream, double-buffered
+                   against the batch kernel on a compute stream, and D2H of
+                   each chunk's CRCs: the copy engine and the kernel overlap;
+      h2d_only  -- the same chunked H2D alone (this link's measured ceiling);
+      zero_copy -- one batch call on the pinned buffer's device alias: the
+                   kernel reads the bytes over PCIe, no staging copy.
+
+    Beside them the host CPU over the same pinned bytes (the product's
+    streaming API on the box's cores, and the oracle), so the crossover is
+    in the line.  The CRCs are compared after the headline (e2e_finish)."""
+    import ctypes
+    from mercury_amd import gpu as G
+    method, count, length, seed, _ = CONFIGS["metric"]
+    chunk = 128 << 20
+    total = count * length
+    nchunks, per = total // chunk, chunk // length
+    G.prepare(method)
+    host = torch.empty(total, dtype=torch.uint8, pin_memory=True)
+    stage = torch.empty(chunk + 64, dtype=torch.uint8, device=dev)
+    for i in range(nchunks):  # the headline's bytes (same splitmix stream), made on the device
+        G.fill_splitmix(stage, seed, first_word=i * chunk // 8)
+        host[i * chunk:(i + 1) * chunk].copy_(stage[:chunk])
+    torch.cuda.synchronize()
+    del stage
+    dbuf = [torch.empty(chunk + 64, dtype=torch.uint8, device=dev) for _ in range(2)]
+    dout = [torch.empty(per, dtype=torch.int32, device=dev) for _ in range(2)]
+    hout = torch.empty(count, dtype=torch.int32, pin_memory=True)
+    zout = torch.empty(count, dtype=torch.int32, device=dev)
+    s_copy, s_comp = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
+
+    def staged():
+        copied = [torch.cuda.Event() for _ in range(2)]
+        free = [torch.cuda.Event() for _ in range(2)]
+        for e in free:
+            e.record(s_comp)
+        for i in range(nchunks):
+            b = i % 2
+            s_copy.wait_event(free[b])  # the kernel is done with buffer b
+            with torch.cuda.stream(s_copy):
+                dbuf[b][:chunk].copy_(host[i * chunk:(i + 1) * chunk], non_blocking=True)
+                copied[b].record(s_copy)
+            s_comp.wait_event(copied[b])
+            G.checksum_fixed(method, dbuf[b], length, count=per, out=dout[b], stream=s_comp)
+            with torch.cuda.stream(s_comp):
+                hout[i * per:(i + 1) * per].copy_(dout[b], non_blocking=True)
+            free[b].record(s_comp)
+
+    def h2d_only():
+        with torch.cuda.stream(s_copy):
+            for i in range(nchunks):
+                dbuf[i % 2][:chunk].copy_(host[i * chunk:(i + 1) * chunk], non_blocking=True)
+
+    hip = _hip()
+    alias = ctypes.c_void_p()
+    zc_err = hip.hipHostGetDevicePointer(ctypes.byref(alias), ctypes.c_void_p(host.data_ptr()), 0)
+    lib = G._lib()
+
+    def zero_copy():
+        rc = lib.mchecksum_gpu_checksum_fixed(method.encode(), alias.value, length, length, count, zout.data_ptr(),
+                                              s_comp.cuda_stream)
+        if rc:
+            raise G.GpuChecksumError(f"zero-copy batch call rc={rc}")
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        laps = []
+        for _ in range(max(1, args.e2e_reps)):
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize()
+            laps.append(time.perf_counter() - t0)
+        med = float(np.median(laps))
+        return {"GiB_s": round(total / med / 2**30, 2), "GB_s": round(total / med / 1e9, 2),
+                "pcie_frac": round(total / med / 1e9 / PCIE_GEN5_X16_GBS, 4), "ms": round(med * 1e3, 2),
+                "ms_min": round(min(laps) * 1e3, 2), "ms_max": round(max(laps) * 1e3, 2), "reps": len(laps)}
+
+    rec = {"workload": f"{method} over {count} x {length} B payloads in pinned host memory (the headline's bytes), "
+                       "CRCs back in host memory",
+           "pcie_spec_GB_s": PCIE_GEN5_X16_GBS,
+           "staged": dict(timed(staged), chunk_bytes=chunk, streams="copy + compute, double-buffered"),
+           "h2d_only": dict(timed(h2d_only), chunk_bytes=chunk)}
+    rec["staged"]["of_h2d_only"] = round(rec["h2d_only"]["ms"] / rec["staged"]["ms"], 4)
+    if zc_err == 0:
+        rec["zero_copy"] = dict(timed(zero_copy), how="hipHostGetDevicePointer alias of the pinned buffer, one call")
+    else:
+        rec["zero_copy"] = {"skipped": f"hipHostGetDevicePointer error {zc_err}"}
+    # host CPU over the same pinned bytes: the first 4096 payloads (256 MiB)
+    cpu_n = 4096
+    hb = host.numpy()
+    threads = _cpu_threads()
+    cpu = {"sample": f"the first {cpu_n} payloads ({cpu_n * length >> 20} MiB) of the same pinned buffer",
+           "cores": threads}
+    try:
+        pv = product_batch(method, hb[:cpu_n * length], threads, count=cpu_n, length=length)
+        cpu["product_crcs"] = pv
+        cpu["product_GiB_s"] = round(_rate(lambda: product_batch(method, hb[:cpu_n * length], threads, count=cpu_n,
+                                                                 length=length), cpu_n * length), 2)
+    except OSError as e:
+        cpu["product_GiB_s"] = None
+        cpu["product_note"] = f"product CPU path not timed: {e}"
+    rec["cpu_same_bytes"] = cpu
+    rec["_crcs"] = {"staged": hout.numpy().view(np.uint32).copy(), "zero_copy": G.as_unsigned(zout)
+                    if zc_err == 0 else None}
+    rec["_host"] = hb
+    rec["_shape"] = (method, count, length, cpu_n)
+    del dbuf, dout
+    torch.cuda.synchronize()
+    return rec
+
+
+def _rate(fn, nbytes, budget_s=0.5):
+    """GiB/s of fn over nbytes: passes until budget_s, at least 3."""
+    n, t0 = 0, time.perf_counter()
+    while True:
+        fn()
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s and n >= 3:
+            return n * nbytes / el / 2**30
+
+
+def e2e_finish(rec, got, args):
+    """The e2e CRCs against the headline's device-resident CRCs (every
+    payload; those are oracle-checked in `parity`) and, independently, the
+    oracle over sampled payloads of the pinned host bytes themselves."""
+    from oracle import oracle as O
+    method, count, length, cpu_n = rec.pop("_shape")
+    crcs, hb = rec.pop("_crcs"), rec.pop("_host")
+    notes, ok = [], True
+    for leg in ("staged", "zero_copy"):
+        c = crcs.get(leg)
+        if c is None:
+            continue
+        bad = int(np.count_nonzero(c.astype(np.uint64) != np.asarray(got[:count]).astype(np.uint64)))
+        ok &= bad == 0
+        notes.append(f"{leg}: {count - bad}/{count} equal the device-resident CRCs")
+    rng = np.random.default_rng(0xE2E)
+    idx = sorted(set([0, count - 1]) | set(int(i) for i in rng.integers(0, count, 62)))
+    obad = sum(int(crcs["staged"][i]) != O.crc(method, hb[i * length:(i + 1) * length]) for i in idx)
+    ok &= obad == 0
+    notes.append(f"{len(idx) - obad}/{len(idx)} sampled payloads of the pinned bytes equal the oracle")
+    cpu = rec["cpu_same_bytes"]
+    pv = cpu.pop("product_crcs", None)
+    if pv is not None:
+        n = len(pv)
+        pbad = int(np.count_nonzero(pv.astype(np.uint64) != crcs["staged"][:n].astype(np.uint64)))
+        ok &= pbad == 0
+        notes.append(f"product CPU path: {n - pbad}/{n} equal the staged GPU CRCs")
+    rec["parity"] = ("bit-exact: " if ok else "MISMATCH: ") + "; ".join(notes)
+    if not args.no_cpu_baseline:
+        # the oracle on the same sample, on the same cores (kind "port": the
+        # reference's own mchecksum is absent)
+        sub = hb[:cpu_n * length]
+        threads = cpu["cores"]
+        cpu["oracle_GiB_s"] = round(_rate(lambda: O.batch_fixed(method, sub, length, length, cpu_n,
+                                                                variant="sse42", nthreads=threads),
+                                          cpu_n * length), 2)
+        cpu["oracle_variant"] = "x86 SSE4.2 crc32 instruction"
+    return rec
+
+
+def _cpu_threads():
+    """Every CPU this process may use, capped by the cgroup quota (cpu_baseline's rule)."""
+    affinity = len(os.sched_getaffinity(0))
+    quota = _cpu_quota()
+    return max(1, min(256, affinity, int(quota[0]) if quota else affinity))
 
 
 def c5_parity(got, firsts, samples):

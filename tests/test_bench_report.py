@@ -148,3 +148,45 @@ def test_two_rank_line_flags_a_wrong_share(name):
     """A wrong CRC in rank 1's share reads as a mismatch, not as bit-exact."""
     res = _run(name, corrupt=True)
     assert res["parity"].startswith("MISMATCH 1/") and "across all 2 shares" in res["parity"], res["parity"]
+
+
+def _e2e_record(O, count=64, length=4096, cpu_n=16, seed=0x4D43310000000005):
+    """An e2e record as bench.run_e2e leaves it for e2e_finish, built on the
+    CPU: the host bytes, the legs' CRCs (oracle values standing in for the
+    GPU's) and the product CPU path's CRCs of the first cpu_n payloads."""
+    hb = O.splitmix_bytes(count * length, seed)
+    want = O.batch_fixed("crc32c", hb, length, length, count).astype(np.uint32)
+    rec = {"staged": {}, "h2d_only": {}, "zero_copy": {},
+           "cpu_same_bytes": {"cores": 1, "product_crcs": want[:cpu_n].astype(np.uint64)},
+           "_crcs": {"staged": want.copy(), "zero_copy": want.copy()}, "_host": hb,
+           "_shape": ("crc32c", count, length, cpu_n)}
+    return rec, want
+
+
+def test_e2e_finish_bit_exact_and_detects_a_wrong_crc():
+    """bench.e2e_finish: both host-memory legs are compared with the
+    device-resident CRCs on every payload and with the oracle on sampled
+    payloads of the host bytes; a single wrong CRC turns the verdict."""
+    sys.path.insert(0, ROOT)
+    import bench
+    from oracle import oracle as O
+
+    class A:
+        no_cpu_baseline = False
+
+    rec, want = _e2e_record(O)
+    out = bench.e2e_finish(rec, want.copy(), A())
+    assert out["parity"].startswith("bit-exact"), out["parity"]
+    assert "64/64 equal the device-resident" in out["parity"]
+    assert out["cpu_same_bytes"]["oracle_GiB_s"] > 0
+    assert not any(k.startswith("_") for k in out)
+
+    rec, want = _e2e_record(O)
+    rec["_crcs"]["zero_copy"][17] ^= 1
+    out = bench.e2e_finish(rec, want.copy(), A())
+    assert out["parity"].startswith("MISMATCH") and "zero_copy: 63/64" in out["parity"]
+
+    rec, want = _e2e_record(O)
+    rec["_crcs"]["staged"][0] ^= 0x80000000  # also sampled by the oracle leg
+    out = bench.e2e_finish(rec, want.copy(), A())
+    assert out["parity"].startswith("MISMATCH")

@@ -11,6 +11,9 @@ from tools_shapes import SHAPES
 ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="c3")
 ap.add_argument("--iters", type=int, default=5)
+# fixed layouts: launch i reads copy i % R of R equal batches at distinct
+# addresses (bench.py --rotate: C2's 256 MiB is Infinity-Cache sized)
+ap.add_argument("--rotate", type=int, default=1)
 a = ap.parse_args()
 method, count, length, seed = SHAPES[a.config]
 if a.config == "msgs":  # bench.py's msgs layout: HG header (network-order payload CRC) at 16, payload from 20
@@ -58,9 +61,14 @@ elif length is None:
     offs = torch.from_numpy(off.astype(np.int64)).cuda()
     run = lambda: G.checksum_offsets(method, data, offs)
 else:
-    data = torch.empty(count * length + 64, dtype=torch.uint8, device="cuda")
-    G.fill_splitmix(data, seed)
-    run = lambda: G.checksum_fixed(method, data, length, count=count)
+    datas = [torch.empty(count * length + 64, dtype=torch.uint8, device="cuda") for _ in range(a.rotate)]
+    for d in datas:
+        G.fill_splitmix(d, seed)
+    it = [0]
+
+    def run():
+        G.checksum_fixed(method, datas[it[0] % len(datas)], length, count=count)
+        it[0] += 1
 for _ in range(a.iters):
     run()
 torch.cuda.synchronize()
