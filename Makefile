@@ -25,7 +25,7 @@ QFAULTLIB := $(BUILD)/libmchecksum_qfault.so
 STAMP_SRCS := $(sort $(wildcard $(CSRC)/*.c $(CSRC)/*.h $(CSRC)/*.hip include/*.h))
 STAMP     := $(BUILD)/src_stamp.o
 
-all: $(LIB) $(BENCHLIB) oracle $(BUILD)/c1_bench $(QFAULTLIB) $(BUILD)/libcpu_batch.so
+all: $(LIB) $(BENCHLIB) oracle $(BUILD)/c1_bench $(QFAULTLIB) $(BUILD)/libcpu_batch.so $(BUILD)/hg_verify_consumer
 
 $(BUILD) $(LIBDIR):
 	mkdir -p $@
@@ -78,6 +78,15 @@ $(BUILD)/libcpu_batch.so: tools/cpu_batch.c include/mchecksum.h $(LIB) | $(BUILD
 	$(CC) -O2 -std=c11 -Wall -Wextra -fPIC -shared -fvisibility=hidden -Iinclude $< -o $@ -L$(LIBDIR) -lmchecksum \
 	  -lpthread -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)'
 
+# A compiled consumer of the batch ABI, found
+# through cmake/mchecksum-config.cmake as Mercury would; run by
+# tests/test_gpu_consumer.py on the GPU and tests/test_cmake_consumer.py here.
+$(BUILD)/hg_verify_consumer: tests/native/hg_verify_consumer.c tests/native/hg_consumer/CMakeLists.txt \
+		include/mchecksum.h include/mchecksum_gpu.h cmake/mchecksum-config.cmake $(LIB) | $(BUILD)
+	cmake -S tests/native/hg_consumer -B $(BUILD)/hg_consumer -Dmchecksum_DIR=$(CURDIR)/cmake > /dev/null
+	cmake --build $(BUILD)/hg_consumer > /dev/null
+	cp $(BUILD)/hg_consumer/hg_verify_consumer $@
+
 # CPU-only artefacts (no hipcc needed): streaming API for host tests.
 cpu: $(LIBDIR)/libmchecksum_cpu.so
 $(LIBDIR)/libmchecksum_cpu.so: $(COBJS) | $(LIBDIR)
@@ -98,7 +107,7 @@ clean:
 
 # A/B variants of the batch kernels (tools/ab_variants.py).  Each is a full
 # libmchecksum built with different tuning macros.
-VARIANTS ?= base:-DMCK_RING=4 nib:-DMCK_CRC64_P6=0
+VARIANTS ?= base:
 variants: $(COBJS) $(BUILD)/mchecksum_gpu_ext.o | $(BUILD)
 	mkdir -p $(BUILD)/variants
 	@for v in $(VARIANTS); do n=$${v%%:*}; f=$$(echo $${v#*:} | tr , " "); \

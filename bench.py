@@ -147,10 +147,14 @@ def main():
     dist_on = env_world is not None
     ndev = torch.cuda.device_count()  # (counting devices does not initialise the GPU)
     if dist_on:
-        # one GPU per rank: a run with more ranks than GPUs is refused (round 4
-        # mapped ranks modulo the count); only the gloo rehearsal may share one
-        if args.backend == "nccl" and (local >= ndev or world > ndev):
-            sys.exit(f"bench.py: {world} ranks (LOCAL_RANK {local}) but {ndev} GPU(s) visible: one GPU per rank")
+        # one GPU per rank: a node with more ranks than GPUs is refused (round 4
+        # mapped ranks modulo the count); only the gloo rehearsal may share one.
+        # Per node (LOCAL_WORLD_SIZE): a multi-node run has more ranks in all
+        # than one node has GPUs.
+        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", world))
+        if args.backend == "nccl" and (local >= ndev or local_world > ndev):
+            sys.exit(f"bench.py: {local_world} ranks on this node (LOCAL_RANK {local}) but {ndev} GPU(s) visible: "
+                     "one GPU per rank")
         torch.cuda.set_device(local if args.backend == "nccl" else local % max(ndev, 1))
         # The communication libraries may print connection notices on file
         # descriptor 1 (gloo's "[Gloo] Rank 0 is connected to ..."), which
@@ -175,16 +179,21 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
     coll_dev = dev if args.backend == "nccl" else torch.device("cpu")
-    # every rank's PCI address, gathered into the line: N distinct GPUs took part
-    pci = [float(x) for x in pci_address(torch, dev)]
+    # every rank's PCI address and host, gathered into the line: N distinct
+    # GPUs took part (the same PCI address on two hosts is two GPUs)
+    import socket
+    import zlib
+    host = socket.gethostname()
+    pci = [float(x) for x in pci_address(torch, dev)] + [float(zlib.crc32(host.encode()))]
     if dist_on:
         pt = torch.tensor(pci, dtype=torch.float64, device=coll_dev)
         allp = [torch.empty_like(pt) for _ in range(world)]
         dist.all_gather(allp, pt)
-        pcis = [pci_string(p.tolist()) for p in allp]
+        keys = [tuple(p.tolist()) for p in allp]
     else:
-        pcis = [pci_string(pci)]
-    if args.backend == "nccl" and len(set(pcis)) != world:
+        keys = [tuple(pci)]
+    pcis = [pci_string(k[:3]) for k in keys]
+    if args.backend == "nccl" and len(set(keys)) != world:
         sys.exit(f"bench.py: ranks share a GPU ({pcis}): one GPU per rank")
 
     c5_strong = None
@@ -1129,7 +1138,7 @@ def share_firsts(plan, layout, world, count0):
 def pmc_traffic(config, world, alg_bytes):
     """roofline.traffic: HBM bytes per launch cannot be counted inside this
     process -- they come from the committed rocprofv3 FETCH_SIZE / WRITE_SIZE
-    passes of this config (tools/gpu_r03.sh PART=pmc ->
+    passes of this config (tools/gpu_pass.sh PART=pmc ->
     profiles/pmc_traffic_<config>.json).  At N > 1 the profile (one GPU, the
     whole batch) is scaled to rank 0's share by its traffic/algorithmic
     ratio.  (None, reason) when there is no profile."""

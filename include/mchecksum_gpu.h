@@ -39,11 +39,20 @@
  * with calls in flight follows the HIP rules for the memory those calls use;
  * the library itself keeps no per-stream state.
  *
- * Fail closed: every wait in the work queue is bounded.  A launch in which a
- * wait gives up (a protocol fault; 0 in every test run) adds 1 to the error
- * word set with mchecksum_gpu_set_error_word(), adds `count` to the mismatch
- * counter of a verify call and marks every payload it cannot vouch for with
- * status 1, so unhashed bytes never read as verified.
+ * Fail closed: every wait on the device is bounded, and so is every call.  A
+ * wait gives up after 1 s of real time (time the wave spends switched out of
+ * the GPU does not count); once one wait of a call has given up, every other
+ * wait of that call gives up at once (the launch's abort flag; a segments
+ * call whose scan gave up hashes nothing more), so a call that meets any
+ * number of stalls still returns within about one deadline.  A call in which
+ * a wait gave up (a protocol fault; 0 in every test run) adds 1 -- once per
+ * call -- to the error word set with mchecksum_gpu_set_error_word(), adds
+ * `count` to the mismatch counter of a verify call and marks every payload it
+ * cannot vouch for with status 1, so unhashed bytes never read as verified.
+ *
+ * Settings: the MCHECKSUM_* environment variables (variants, log level, the
+ * MCHECKSUM_GPU_* launch-policy overrides of the A/B tools) are read once,
+ * at the library's first use, never on the call path.
  *
  * There is NO host fallback: without a usable HIP device every call returns
  * MCHECKSUM_GPU_ENODEV.
@@ -228,6 +237,12 @@ mchecksum_gpu_set_error_word(uint32_t *dev_word);
 /* Human-readable text for the last error on this thread. */
 MCHECKSUM_PUBLIC const char *
 mchecksum_gpu_last_error(void);
+
+/* Re-read the MCHECKSUM_* environment settings (normally read once, at first
+ * use) for calls made from now on -- for tests and tuning tools that change
+ * the environment between calls; calls already made are not affected. */
+MCHECKSUM_PUBLIC void
+mchecksum_gpu_reload_settings(void);
 
 /* Diagnostics: the number of work-queue protocol faults the batch kernels
  * counted on the current device since the library was loaded (0 in a

@@ -24,7 +24,7 @@ GPU_SYMBOLS = ("mchecksum_gpu_available", "mchecksum_gpu_prepare", "mchecksum_gp
                "mchecksum_gpu_lanes_per_payload", "mchecksum_gpu_last_error", "mchecksum_gpu_segments_work_size",
                "mchecksum_gpu_checksum_segments", "mchecksum_gpu_verify_core_headers",
                "mchecksum_gpu_queue_faults", "mchecksum_gpu_set_error_word", "mchecksum_gpu_checksum_xdr",
-               "mchecksum_gpu_queue_stats")
+               "mchecksum_gpu_queue_stats", "mchecksum_gpu_reload_settings")
 CORE_HEADER_REQUEST, CORE_HEADER_RESPONSE = 0, 1
 # XDR schema field kinds (include/mchecksum_gpu.h)
 XDR_INT, XDR_OPAQUE, XDR_OPAQUE_LEN, XDR_RAW, XDR_RAW_LEN, XDR_SKIP_IF_ZERO = 0, 1, 2, 3, 4, 5
@@ -94,8 +94,16 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     L.mchecksum_gpu_checksum_xdr.argtypes = [c_char_p, ctypes.POINTER(XdrField), c_size_t, c_void_p, c_void_p,
                                              c_size_t, c_void_p, c_void_p, c_void_p]
     L.mchecksum_gpu_checksum_xdr.restype = c_int
+    L.mchecksum_gpu_reload_settings.argtypes = []
+    L.mchecksum_gpu_reload_settings.restype = None
     _lib = L
     return L
+
+
+def reload_settings() -> None:
+    """Have libmchecksum re-read its MCHECKSUM_* environment settings, which it
+    otherwise reads once per process (tests and A/B tools that change them)."""
+    load_library().mchecksum_gpu_reload_settings()
 
 
 # The sources libmchecksum is built from (the Makefile's STAMP_SRCS): their

@@ -16,25 +16,13 @@
 
 namespace {
 
-// Build-time tuning knobs (A/B builds: tools/ab_variants.py); defaults are
-// the measured best.
-#ifndef MCK_BLOCK
-#define MCK_BLOCK 1024
-#endif
-#ifndef MCK_RING
-#define MCK_RING 4
-#endif
-#ifndef MCK_BITOP3
-#define MCK_BITOP3 1
-#endif
-constexpr int kBlock = MCK_BLOCK;  // 1024 = 16 waves: 4 per SIMD
-constexpr int kRing = MCK_RING;  // dwordx4 pieces in flight per lane
+// Tuning constants are the measured best (their A/Bs: DESIGN.md and
+// HISTORY.md; losing alternatives are not kept in the source).
+constexpr int kBlock = 1024;  // 16 waves: 4 per SIMD
+constexpr int kRing = 4;      // dwordx4 pieces in flight per lane
 // Offsets batches (one payload per wave, ~32 KiB average) want a deeper ring:
 // 8 measured +4% over 4 on C4, while 8 costs 1-5% on the aligned batches.
-#ifndef MCK_RING_OFFSETS
-#define MCK_RING_OFFSETS 8
-#endif
-constexpr int kRingOff = MCK_RING_OFFSETS;
+constexpr int kRingOff = 8;
 
 // CRC-32C LDS map: [0,128K) main byte tables x32 copies; then op nibble
 // tables; then the two-level combine operators (crc_gpu_layout.h lv, 8 KiB).
@@ -55,200 +43,47 @@ template <bool LIGHT>
 struct Tab32 {
     const uint8_t *lds;
 };
-// CRC-64 LDS map.  A 64-bit state is looked up by nibble: the 8 low-nibble
-// tables are replicated 32x (entry v at v*256 B, lane copy at (lane%32)*8 B;
-// the address is one v_and_b32_sdwa of the nibble into the lane-copy register,
-// f64x_byte below), the 8
-// high-nibble tables are NOT replicated: entry v sits at v*16 B, so the masked
-// byte (v << 4) is its own address and the 16 entries fall on 16 distinct bank
-// pairs of ds_read_b64 (lanes that share an entry broadcast) -- conflict-free
-// without copies.  Tables p and p+4 share a 256-B block (p+4 at +8 B).  Then
-// the combine operators (nibble tables, 2 KiB each).
-//
-// MCK_CRC64_P6=1 instead looks a 64-bit word up in 12 tables (pack f5/f6):
-// bits 3..7 of each byte index a 32-entry table at 8-B stride -- one 256-B
-// row, entry v on bank pair v, conflict-free without copies, address =
-// (byte & 0xF8) --, and bits 0..2 of bytes i and i+4, gathered into one
-// 6-bit index by one shift + bit-select for all four, a 64-entry table
-// replicated 32x (entry v at v*256 B + lane copy, 16 KiB per table).  Three
-// quarters of the LDS reads of the nibble form; the combine operators then
-// move to global memory so two workgroups per CU still fit.
-#ifndef MCK_CRC64_P6
-#define MCK_CRC64_P6 1
-#endif
-#if MCK_CRC64_P6
+// CRC-64 LDS map.  A 64-bit word is looked up in 12 tables (pack f5 / f6,
+// crc_gpu_layout.h): bits 3..7 of each of its 8 bytes index a 32-entry table
+// at 8-B stride -- one 256-B row, entry v on bank pair v, so distinct entries
+// never share a bank and equal ones broadcast: conflict-free without lane
+// copies, and the address is (byte & 0xF8) itself --, and bits 0..2 of bytes i
+// and i + 4, gathered into one 6-bit index by one shift + bit-select for all
+// four, index a 64-entry table replicated 32x (entry v at v*256 B + lane copy
+// (lane % 32)*8: 16 KiB per table).  Then the combine operators (16 nibble
+// tables, 2 KiB each).  (Round 1's 16-lookup nibble form needed a third more
+// LDS reads; 11 lookups over 7-bit tables, a wide-row map with cheaper address
+// ops and two workgroups per CU all measured slower: HISTORY.md.)
 constexpr uint32_t kL64P5 = 0;
 constexpr uint32_t kL64P6 = 8 * 256;
 constexpr uint32_t kL64Main = kL64P6 + 4 * 16384;
-#else
-constexpr uint32_t kL64Hi = 32768;
-constexpr uint32_t kL64Main = kL64Hi + 4 * 256;
-#endif
 constexpr uint32_t kL64Bytes = kL64Main + CRC64_NOPS_MAX * 2048;
-// The 11-lookup fold (kFold11, round 5) for the one-workgroup-per-CU kernels
-// (aligned fixed batches: C3; the merged segment pass).  The 12-lookup fold
-// keeps C3's LDS array ~82% busy (SQ_LDS_IDX_ACTIVE over the launch's cycles,
-// profiles/r05/sq_c3.txt): CRC-64 is LDS-bound, at 2 array cycles per
-// ds_read_b64 and 12 per 8-byte word.  With a whole CU's LDS, bits 0..6 of
-// bytes 6 and 7 and two 7-bit gathers of the low bits go to 7-bit tables
-// replicated 32x (32 KiB each): f5 over bytes 0..5 (6 lookups), 4 x f7, one
-// 6-bit pair table -- 11 lookups per word, 29 VALU instead of 26.  Map:
-//   [512, 2048)        f5[0..5] (256 B each, unreplicated)
-//   [2048, 67584)      f7[0], f7[1] (entry v at v*256 + lane copy*8)
-//   [67584, 79872)     butterfly operators Z^-(16*2^k), k < 6 (kL64Main, as
-//                      in the mixed operator mode)
-//   [79872, 145408)    f7[2], f7[3]
-//   [145408, 161792)   f6b (x32)
-// An address is the lane-copy register (byte 0: copy offset, byte 1: the
-// index, byte 2: the 64 KiB region) plus the DS immediate offset (< 64 KiB).
-enum Fold : int { kFold12 = 0, kFold11 = 1, kFold12W = 2 };
-// kFold12W (round 5): the 12-lookup fold with its addresses formed by ops that
-// issue in ~1.8 cycles (VOP2 AND / v_bitop3 with VGPR operands) instead of
-// SDWA (~2.8; tools/valu_probe.hip).  Bits 3..7 of the even bytes of each
-// half stay in unreplicated 256-B tables (address = x & 0xF8 after a 16-bit
-// shift for bytes 2 and 6); bits 3..7 of the odd bytes are read in place as
-// (x & 0xF800) | lane copy -- entry v at v * 2 KiB, so these four tables are
-// replicated 32x in rows of 2 KiB, interleaved (slot k at +256 k); the pair
-// index of t's byte 1 is (t & 0x3F00) | lane copy, the other three stay SDWA.
-//   [0, 65536)        rows v = 0..31 of 2 KiB: slots 0..3 = f5[1], f5[3],
-//                     f5[5], f5[7] (x32); [1024, 2048) of row 0: f5[0, 2, 4, 6]
-//   [67584, 79872)    butterfly operators (kL64Main, the mixed operator mode)
-//   [79872, 145408)   f6[0..3] (x32), region 1 of the lane registers
-constexpr uint32_t kWUnrep = 1024;
-constexpr uint32_t kWF6 = kL64Main + 6 * 2048;
-constexpr uint32_t kWBytes = kWF6 + 4 * 16384;
-static_assert(kWF6 - 65536 + 3 * 16384 < 65536, "f6 offsets fit the DS immediate");
-constexpr uint32_t kF11F5 = 512;
-constexpr uint32_t kF11F7a = 2048;
-constexpr uint32_t kF11F7c = kL64Main + 6 * 2048;
-constexpr uint32_t kF11F6 = kF11F7c + 2 * 32768;
-constexpr uint32_t kF11Bytes = kF11F6 + 16384;
-static_assert(kF11F7a + 2 * 32768 == kL64Main, "butterflies follow f7[0..1]");
-static_assert(kF11F7c == 65536 + 14336 && kF11F6 == 131072 + 14336, "region offsets in the lane registers");
-// CRC-64 is LDS/VALU-bound (table reads and their XOR tree); two 1024-thread
-// workgroups per CU (8 waves/SIMD) hide the LDS latency.  MCK_CRC64_SPLIT=1
-// (implied by MCK_CRC64_P6) reads the combine operators (touched once per
-// payload) from global memory instead of LDS on the aligned path.
-#ifndef MCK_CRC64_SPLIT
-#define MCK_CRC64_SPLIT 0
-#endif
-#ifndef MCK_BLOCK64
-#define MCK_BLOCK64 1024
-#endif
-// Fold the next data word into the table-XOR tree (its 17th input slot is
-// free) and run the aligned step loop without per-step bounds tests.
-#ifndef MCK_LA64
-#define MCK_LA64 1
-#endif
-
-// Two workgroups per CU on the CRC-64 offsets path as well, with a 4-deep ring
-// so its loop fits 64 VGPRs: C4-layout CRC-64 +10% over one workgroup with
-// ring 8 (a ring of 8 at two workgroups spills: -42%; ring 4 on the CRC-32C
-// offsets path: -3%) -- profiles/r01/ab11_crc64_offsets_two.log.
-#ifndef MCK_CRC64_OFF_TWO
-#define MCK_CRC64_OFF_TWO 1
-#endif
-// Under MCK_CRC64_P6 the offsets path cannot read all its combine operators
-// from global memory (a dependent chain of 8 operator applications per
-// payload: C4-layout CRC-64 ran 21% slower) and all of them in LDS leave room
-// for only one workgroup per CU.
-// MCK_CRC64_OFF_MIX=1 instead keeps only the six butterfly operators in LDS
-// (12 KiB: 79.9 KiB in all) and reads Z^-8 and the tail operator, the two
-// ends of the chain, from global memory: two workgroups per CU again, +6% on
-// C4-layout CRC-64 (profiles/r01/ab20_crc64_offsets_mix.log).
-#ifndef MCK_CRC64_OFF_MIX
-#define MCK_CRC64_OFF_MIX 1
-#endif
-constexpr bool kCrc64OffMix = MCK_CRC64_P6 && MCK_CRC64_OFF_MIX;
-constexpr bool kCrc64OffTwo = (MCK_CRC64_OFF_TWO && !MCK_CRC64_P6) || kCrc64OffMix;
-constexpr int kRingOff64 = kCrc64OffTwo ? 4 : kRingOff;
-// where the CRC-64 combine operators live: all in LDS, all in global memory,
-// or the butterflies (ops 1..6) in LDS and the rest global
+// Where the CRC-64 combine operators live: all in LDS (one 1024-thread
+// workgroup per CU: the aligned batches and the merged segment pass), all in
+// global memory (the XDR throughput kernel), or the six butterflies
+// Z^-(16*2^k) in LDS and Z^-8 and the tail operators -- the two ends of the
+// offsets path's dependent chain -- in global memory (the offsets path: two
+// workgroups per CU at 79.9 KiB each, +6-8% on C4-layout CRC-64 over either
+// pure form, profiles/r01/ab20_crc64_offsets_mix.log).
 enum OpsMode : int { kOpsLds = 0, kOpsGlobal = 1, kOpsMix = 2 };
 
-// The aligned CRC-64 loop runs one 1024-thread workgroup per CU (round 4;
-// round 3 ran two): 128 VGPRs instead of 64 (no spills, room for a deeper
-// load ring, MCK_RING64) and, with the LDS of a whole CU, the combine
-// operators in LDS beside the tables -- half the waves to hide the LDS
-// latency, which measured as well: C3 1.3786 -> 1.3421 ms (-2.6%), 1 and 1024
-// x 4 KiB calls 10.4 -> 9.2 / 9.6 us, one process, 8 rounds
-// (profiles/r04/ab_c3_onewg.log: "onewglds"; one WG with the operators still in
-// global memory, "onewg", gave -0.9% -- round 3's +0.4% / +1.4% A/Bs,
-// profiles/r03/ab_crc64_one_wg_c3*.log).  The merged segment pass runs the
-// same shape (mchecksum_gpu_ext.hip).  MCK_CRC64_ONE_WG=0 builds the two.
-#ifndef MCK_CRC64_ONE_WG
-#define MCK_CRC64_ONE_WG 1
-#endif
-#ifndef MCK_RING64
-#define MCK_RING64 MCK_RING
-#endif
-// ... and with one workgroup per CU the combine operators fit in LDS beside
-// the tables (kL64Bytes), as in the merged segment pass (round 4).
-#ifndef MCK_CRC64_ONE_WG_OPS_LDS
-#define MCK_CRC64_ONE_WG_OPS_LDS 1
-#endif
-// MCK_CRC64_FOLD11=1 builds the aligned one-workgroup-per-CU CRC-64 kernels
-// with the 11-lookup fold (butterflies in LDS, Z^-8 from global memory).  Off:
-// bit-exact (GPU parity suite green with it) but C3 -4.9% in one process
-// (1.3490 vs 1.2865 ms median, g64k -1.9%, g16k/g4k +-0.5%;
-// profiles/r05/ab_fold11.log).  Its counters (profiles/r05/sq_c3_fold11.txt)
-// show why: LDS-array cycles -8.2% (SQ_LDS_IDX_ACTIVE) and LDS issue waits
-// -37%, but VALU instructions +10.9% and shader cycles +6.2% -- the fold is
-// bound by VALU issue (26 VALU per 8-byte word at ~4 cycles each per SIMD:
-// ~90% of the launch's cycles), not by the LDS array, so a lookup traded for
-// three gather ops loses.
-#ifndef MCK_CRC64_FOLD11
-#define MCK_CRC64_FOLD11 0
-#endif
-// MCK_CRC64_TWO_MIX=1 (with MCK_CRC64_ONE_WG=0): the two-workgroup aligned
-// kernels keep the butterfly operators in LDS (mixed mode, 79.9 KiB each).
-#ifndef MCK_CRC64_TWO_MIX
-#define MCK_CRC64_TWO_MIX 0
-#endif
-#ifndef MCK_CRC64_FOLD12W
-#define MCK_CRC64_FOLD12W 0
-#endif
-// MCK_CRC64_L8 (late round 5): aligned CRC-64 payloads at 64 lanes run with
-// ONE 64-bit state per lane -- 8 bytes per lane and step, a 512-B wave load,
-// the stride tables of the 32-lane pack (16 * 32 = 512 B) -- so the loop fits
-// 64 VGPRs and two workgroups share a CU (8 waves/SIMD, the butterflies in each
-// workgroup's LDS: 78 KiB).  tools/fold_probe.hip's steady-state series
-// promised it: the one-state loop at two workgroups per CU streamed 4 GiB in
-// 0.6433 ms against 0.6778 ms for the probe's two-state loop at one (+5.4%).
-// Built, it is bit-exact (the CRC-64 parity, split, full-shape and golden GPU
-// suites pass with it: profiles/r05/l8/) but slower than the batch kernel it
-// would replace, which already streams faster than the probe's two-state loop:
-// C3 1.3614 vs 1.3018 ms (-4.4%; ring 4: 1.3800), 64-lane payloads
-// not split 0.2141 vs 0.1820 ms (tools/ab_variants.py --series, one process).
-// Off.
-#ifndef MCK_CRC64_L8
-#define MCK_CRC64_L8 0
-#endif
+// Launch shape per kernel.  CRC-32C: one 1024-thread workgroup per CU (the
+// replicated tables take 140 KiB), or the light layout's 256-thread
+// workgroups, 8 per CU.  CRC-64 aligned and generic fixed batches: one
+// 1024-thread workgroup per CU with every operator in LDS (round 4: C3 -2.6%
+// in time against two workgroups per CU with the operators in global memory,
+// profiles/r04/ab_c3_onewg.log).  CRC-64 offsets batches: two workgroups per
+// CU, the mixed operator placement and a 4-deep ring so the loop fits 64
+// VGPRs (a ring of 8 at two workgroups spills: -42%).
 template <int W, int MODE, bool LIGHT = false, int LG = -1>
 struct Shape {
-    static constexpr bool l8 = W == 64 && MODE == 0 && LG == 6 && !LIGHT && MCK_CRC64_L8 && MCK_CRC64_P6;
-    static constexpr bool two = W == 64 && ((MODE == 0 && (!MCK_CRC64_ONE_WG || l8)) || (MODE == 2 && kCrc64OffTwo));
-    // aligned batches at one workgroup per CU (0 = kFixedAligned): the 11-lookup
-    // or the wide-row fold
-    static constexpr bool one_wg_aligned = W == 64 && MODE == 0 && !two && MCK_CRC64_P6;
-    static constexpr int fold = one_wg_aligned && MCK_CRC64_FOLD11    ? kFold11
-                                : one_wg_aligned && MCK_CRC64_FOLD12W ? kFold12W
-                                                                      : kFold12;
-    static constexpr bool ops_global = W == 64 && MODE == 0 && fold == kFold12 && (MCK_CRC64_SPLIT || MCK_CRC64_P6) &&
-                                       !(MCK_CRC64_ONE_WG && MCK_CRC64_ONE_WG_OPS_LDS) && !MCK_CRC64_TWO_MIX && !l8;
-    static constexpr int block = LIGHT ? kLightBlock : two ? MCK_BLOCK64 : kBlock;
+    static constexpr bool two = W == 64 && MODE == 2;
+    static constexpr int block = LIGHT ? kLightBlock : kBlock;
     static constexpr int blocks_per_cu = LIGHT ? 8 : two ? 2 : 1;
-    static constexpr int ops_mode = ops_global ? kOpsGlobal
-                                    : fold != kFold12 || l8 || (W == 64 && MODE == 2 && kCrc64OffMix) ||
-                                              (W == 64 && MODE == 0 && two && MCK_CRC64_TWO_MIX)
-                                          ? kOpsMix
-                                          : kOpsLds;
-    static constexpr uint32_t lds64_bytes = fold == kFold11            ? kF11Bytes
-                                          : fold == kFold12W          ? kWBytes
-                                          : ops_mode == kOpsGlobal    ? kL64Main
-                                          : ops_mode == kOpsMix       ? kL64Main + 6 * 2048
-                                                                      : kL64Bytes;
+    static constexpr int ops_mode = two ? kOpsMix : kOpsLds;
+    static constexpr uint32_t lds64_bytes = two ? kL64Main + 6 * 2048 : kL64Bytes;
 };
+constexpr int kRingOff64 = 4;
 // single-argument aliases keyed MODE * 16 + LOG2G (a comma inside
 // __launch_bounds__ splits the macro)
 template <int KEY>
@@ -288,11 +123,8 @@ struct BatchArgs {
     uint32_t split_lds;
 };
 // Piece size of a split payload: 256 KiB = 256 steps of the G = 64 loop.
-// (A/B, round 4: 128 KiB pieces +2.9%, 512 KiB +6.8% on C3, profiles/r04/ab_split_piece.log)
-#ifndef MCK_SPLIT_KIB
-#define MCK_SPLIT_KIB 256
-#endif
-constexpr uint64_t kSplitBytes = (uint64_t)MCK_SPLIT_KIB << 10;
+// (A/B, round 4: 128 KiB pieces +2.9%, 512 KiB +6.8% on C3 time, profiles/r04/ab_split_piece.log)
+constexpr uint64_t kSplitBytes = 256u << 10;
 // Payloads per queue chunk whose pieces a workgroup can combine in LDS.
 constexpr uint32_t kSplitAcc = 16;
 
@@ -332,32 +164,11 @@ constexpr uint32_t kSplitAcc = 16;
 // (hipExtLaunchKernel's stop event, queried without blocking, queue_slot), so
 // a workgroup's exit touches no slot line.
 // Bank layout (one counter per 256-B line, 8 KiB per bank, 16 KiB-aligned
-// slots): [0, 8) sub-queue tickets, [8] fault flag of the launch, [9, 17)
-// workgroups exited per sub-queue group, [17] groups exited -- all zeroed by
-// the previous launch on the slot; line 31 of bank 0 counts the slot's
-// completed launches (never zeroed).
-//
-// Completion without an event (late round 5, MCK_SLOT_DONE=1; off by
-// default).  Under rocprofv3 a slot launch's stop event (hipExtLaunchKernel)
-// shows ~4.3 us of idle GPU before the next dispatch on the stream, where a
-// plain launch follows its predecessor with no gap (tools/gap_probe.hip,
-// profiles/r05/gap/; also with the event's system fence disabled or a
-// device-scope release).  With MCK_SLOT_DONE=1 a slot launch reports its own
-// completion instead: each wave, after its last slot access, counts
-// itself out of its workgroup in LDS; the workgroup's last wave counts the
-// workgroup out of its sub-queue group, the group's last one counts the group
-// out of the launch, and the launch's last workgroup bumps the slot's launch
-// count and stores it to the slot's word of host-mapped memory, which the host
-// reads to reap the slot (mchecksum_gpu.hip, slot_idle).  The word is stored
-// while the launch's last waves may still finish their payloads: nothing after
-// it touches the slot.  A launch that never gets there (a fault path that
-// skips the queue) leaves its slot busy for good -- never reused, never wrong.
-// Correct (the slot, queue, thread, fail-closed, split and segment GPU suites
-// pass; tests/test_queue_model.py runs the protocol) but not faster without a
-// profiler: back-to-back series, one process, events vs completion words
-// (tools/ab_variants.py --series, profiles/r05/slot_done/): headline 0.6153 vs
-// 0.6160 ms, C4 1.2388 vs 1.2387, C3 1.3063 vs 1.3072, seg 1.3219 vs 1.3246 --
-// the gap is the profiler's.  So the stop event stays.
+// slots): [0, 8) sub-queue tickets, [8] fault flag of the launch (claimed by
+// its first faulting wave, which reports), [9] abort flag (set by any wave
+// whose bounded wait gave up; every later wait of the launch then gives up at
+// once, so one call spends at most one deadline however many stalls it meets)
+// -- all zeroed by the previous launch on the slot.
 //
 // Exclusivity.  A slot serves one launch at a time: the host hands the queue
 // only to eager launches, each on a slot of its stream's own (launches on one
@@ -374,22 +185,12 @@ constexpr uint32_t kSplitAcc = 16;
 constexpr uint32_t kQSub = 8;
 constexpr uint32_t kQStride = 32;  // u64 words between counters
 constexpr uint32_t kQFault = kQSub;
-constexpr uint32_t kQExitGroup = kQSub + 1;       // + (blockIdx % kQSub)
-constexpr uint32_t kQExitTop = kQExitGroup + kQSub;
-constexpr uint32_t kQBankLines = kQExitTop + 1;  // protocol lines, zeroed before the bank's next use
-constexpr uint32_t kQLaunchLine = 31;            // bank 0 only: the slot's completed launches
+constexpr uint32_t kQAbort = kQSub + 1;
+constexpr uint32_t kQBankLines = kQAbort + 1;  // protocol lines, zeroed before the bank's next use
 constexpr uint64_t kQBankBytes = 8192;
 constexpr uint32_t kQBankWords = (uint32_t)(kQBankBytes / 8);
 constexpr uint32_t kQSlotWords = 2 * kQBankWords;  // slots 2 * kQBankBytes aligned: bank ^ kQBankBytes = the other
-static_assert(kQBankLines * kQStride <= kQBankWords && kQBankLines < kQLaunchLine &&
-                  (kQLaunchLine + 1) * kQStride <= kQBankWords, "bank overflow");
-#ifndef MCK_SLOT_DONE
-#define MCK_SLOT_DONE 0
-#endif
-// The slot pool's base and the host-mapped completion words (one per slot),
-// set once per device by the host (each translation unit has its own copy).
-__device__ unsigned long long *g_mck_qbase;
-__device__ unsigned long long *g_mck_slot_done;
+static_assert(kQBankLines * kQStride <= kQBankWords, "bank overflow");
 // Chunk size: a power of two, about a quarter of a workgroup's fair share
 // of units, between 1 and 32 (C4: 32 units; a 5000-payload batch: 4).
 // Fixed 16 starved half the workgroups of C3's 8192 units at 2 WGs per CU; 32
@@ -397,22 +198,16 @@ __device__ unsigned long long *g_mck_slot_done;
 // the current one is left to take: early enough to hide the fetch (~1.3 us
 // mean), late enough that a workgroup holds little unstarted work when the
 // queue runs dry.
-#ifndef MCK_QCHUNK_MAX_LOG2
-#define MCK_QCHUNK_MAX_LOG2 5
-#endif
-constexpr uint32_t kWgChunkMaxLog2 = MCK_QCHUNK_MAX_LOG2;
+constexpr uint32_t kWgChunkMaxLog2 = 5;
 // Which batches take the queue (profiles/r01/ab12_work_queue.log, medians
 // vs the static split): variable-length (offsets) batches, +4% C4 and +8%
 // C4-layout CRC-64 over the byte-balanced static split, and the large
 // (non-temporal, >= 512 MiB) aligned CRC-32C batches, +2.3% on the headline.
 // Smaller fixed batches and CRC-64 fixed batches keep the static stride:
-// there the queue's fixed costs outweigh the balance (C2 -11%, C3 -5%).
-// MCK_DYN_FIXED=1 builds every throughput kernel with the queue (A/B).
-#ifndef MCK_DYN_FIXED
-#define MCK_DYN_FIXED 0
-#endif
+// there the queue's fixed costs outweigh the balance (C2 -11% warm, -14%
+// with cold lines, profiles/r06/ab_c2cold.log; C3 -5%).
 __host__ __device__ constexpr bool dyn_policy(int width, int mode, bool nt, bool light) {
-    return !light && (mode == 2 || (width == 32 && nt && mode == 0) || MCK_DYN_FIXED);  // 2 = kOffsets
+    return !light && (mode == 2 || (width == 32 && nt && mode == 0));  // 2 = kOffsets
 }
 __device__ __forceinline__ uint32_t chunk_log2(uint64_t n) {
     const uint64_t share = n / (4ull * gridDim.x);
@@ -424,31 +219,22 @@ __device__ __forceinline__ uint32_t chunk_log2(uint64_t n) {
 // Chunk plan: ids [0, nbig) are full chunks of 2^cl units; the last
 // (about one full chunk per workgroup of) units go out as eighth chunks, ids
 // [nbig, nch), so a workgroup that fetches late holds little unstarted work
-// when the queue runs dry (MCK_QTAIL=0: full chunks throughout).  The highest
-// ids are handed out last (every sub-queue counts up), so the small chunks
-// form the tail.
-#ifndef MCK_QTAIL
-#define MCK_QTAIL 1
-#endif
-// Tail chunks are 2^-MCK_QTAIL_SHIFT of a full one, over the last
-// MCK_QTAIL_CHUNKS full chunks per workgroup.  Eighths since round 4
-// (quarters before): never slower in two one-process A/Bs, headline -0.4% /
-// -0.6%, C3 -0.7%, seg -0.7%, C4 +-0 (profiles/r04/ab_qtail.log,
-// ab_round4_knobs.log: "t3"); single-unit tail chunks lost 2.3% on C4 (one
-// fetch per unit), two full chunks per workgroup of tail +0.5% on the headline.
-#ifndef MCK_QTAIL_SHIFT
-#define MCK_QTAIL_SHIFT 3
-#endif
-#ifndef MCK_QTAIL_CHUNKS
-#define MCK_QTAIL_CHUNKS 1
-#endif
+// when the queue runs dry.  The highest ids are handed out last (every
+// sub-queue counts up), so the small chunks form the tail.
+// Tail chunks are 2^-kQTailShift of a full one, over the last full chunk per
+// workgroup.  Eighths since round 4 (quarters before): never slower in two
+// one-process A/Bs, headline -0.4% / -0.6%, C3 -0.7%, seg -0.7%, C4 +-0 in
+// time (profiles/r04/ab_qtail.log, ab_round4_knobs.log: "t3"); single-unit
+// tail chunks lost 2.3% on C4 (one fetch per unit), two full chunks per
+// workgroup of tail +0.5% on the headline.
+constexpr uint32_t kQTailShift = 3;
 struct ChunkPlan {
     uint32_t cl, sl;    // log2 of the full / tail chunk size
     uint64_t nbig, nch, big_end;
     __device__ __forceinline__ explicit ChunkPlan(uint64_t n) {
         cl = chunk_log2(n);
-        sl = MCK_QTAIL && cl >= MCK_QTAIL_SHIFT ? cl - MCK_QTAIL_SHIFT : cl;
-        const uint64_t tail = (uint64_t)MCK_QTAIL_CHUNKS * gridDim.x << cl;
+        sl = cl >= kQTailShift ? cl - kQTailShift : cl;
+        const uint64_t tail = (uint64_t)gridDim.x << cl;
         nbig = n > tail ? (n - tail) >> cl : 0;
         big_end = nbig << cl;
         nch = nbig + ((n - big_end + (1ull << sl) - 1) >> sl);
@@ -459,63 +245,37 @@ struct ChunkPlan {
     }
     __device__ __forceinline__ uint32_t size(uint64_t id) const { return id < nbig ? 1u << cl : 1u << sl; }
 };
-// Split CRC-64 (late round 5): the queue plan of a split launch.  The bulk is
-// ChunkPlan's full chunks of whole payloads in kSplitBytes pieces.  With
-// MCK_SPLIT_TAIL = t > 0 the tail -- ChunkPlan's last full chunk per
-// workgroup -- goes out one payload per chunk in 2^t times smaller pieces
-// (2^tsl = 2^t * 2^psl units), so a workgroup's waves share a tail payload.
-// C3's per-wave trace motivated it (tools/tail_trace.py,
-// profiles/r05/split_tail/): 146 us per 256 KiB piece, waves ending 1166 (p10)
-// to 1278 us (max), ~5.6% of the waves' time idle in the end game, against an
-// 18 us spread on the headline's 37 us units.  With quarter pieces the spread
-// fell to 42 us (1224..1266 us) -- but every piece pays its own combine and
-// Z^n shift, and the waves' busy time grew by as much: C3 1.3161 (quarter) /
-// 1.3186 (half) vs 1.3101 ms (ChunkPlan), one process, 10 rounds.  Off (0):
-// ChunkPlan's layout exactly.  Only when a payload's finer pieces fit one
-// chunk (psl + t <= cl).
-#ifndef MCK_SPLIT_TAIL
-#define MCK_SPLIT_TAIL 0  // log2 of how much finer the tail pieces are
-#endif
+// Split CRC-64: the queue plan of a split launch -- ChunkPlan's layout over
+// count << psl units, unit u = piece (u & (2^psl - 1)) of payload u >> psl.
+// (Late round 5 also tried the tail's payloads in 2-4x finer pieces: the
+// per-wave end spread fell from 111 to 42 us, but every piece pays its own
+// combine and Z^n shift, and C3 lost 0.5%: HISTORY.md.)
 struct SplitPlan {
     uint32_t cl, sl;       // log2 of the full / tail chunk size (units)
-    uint32_t psl, tsl;     // log2 pieces per bulk / tail payload
-    uint64_t nbig, nch, big_end, n, bpay;
+    uint32_t psl;          // log2 pieces per payload
+    uint64_t nbig, nch, big_end, n;
     __host__ __device__ SplitPlan(uint64_t count, uint32_t psl_, uint32_t grid) : psl(psl_) {
-        const uint64_t n0 = count << psl;
-        const uint64_t share = n0 / (4ull * grid);
+        n = count << psl;
+        const uint64_t share = n / (4ull * grid);
         cl = 0;
         while (cl < kWgChunkMaxLog2 && (2ull << cl) <= share) cl++;
-        const bool refine = MCK_SPLIT_TAIL && psl + MCK_SPLIT_TAIL <= cl;
-        tsl = refine ? psl + MCK_SPLIT_TAIL : psl;
-        sl = refine ? tsl : (MCK_QTAIL && cl >= MCK_QTAIL_SHIFT ? cl - MCK_QTAIL_SHIFT : cl);
-        const uint64_t tail = (uint64_t)MCK_QTAIL_CHUNKS * grid << cl;
-        nbig = n0 > tail ? (n0 - tail) >> cl : 0;
+        sl = cl >= kQTailShift ? cl - kQTailShift : cl;
+        const uint64_t tail = (uint64_t)grid << cl;
+        nbig = n > tail ? (n - tail) >> cl : 0;
         big_end = nbig << cl;
-        bpay = big_end >> psl;  // whole payloads (cl >= psl whenever refine)
-        n = refine ? big_end + ((count - bpay) << tsl) : n0;
         nch = nbig + ((n - big_end + (1ull << sl) - 1) >> sl);
     }
     __host__ __device__ uint64_t start(uint64_t id) const { return id < nbig ? id << cl : big_end + ((id - nbig) << sl); }
     __host__ __device__ uint32_t size(uint64_t id) const { return id < nbig ? 1u << cl : 1u << sl; }
-    // unit u: payload *p, piece *q of 2^*lg pieces
-    __host__ __device__ void unit(uint64_t u, uint64_t *p, uint32_t *q, uint32_t *lg) const {
-        if (u < big_end || tsl == psl) {
-            *p = u >> psl;
-            *q = (uint32_t)u & ((1u << psl) - 1u);
-            *lg = psl;
-        } else {
-            const uint64_t v = u - big_end;
-            *p = bpay + (v >> tsl);
-            *q = (uint32_t)v & ((1u << tsl) - 1u);
-            *lg = tsl;
-        }
+    // unit u: piece *q of payload *p
+    __host__ __device__ void unit(uint64_t u, uint64_t *p, uint32_t *q) const {
+        *p = u >> psl;
+        *q = (uint32_t)u & ((1u << psl) - 1u);
     }
     // every chunk holds whole payloads, at most kSplitAcc of them (the
     // in-workgroup combine, split_lds)
     __host__ __device__ bool whole() const {
-        if (psl < 1) return false;
-        if (tsl != psl) return cl >= psl && (1u << (cl - psl)) <= kSplitAcc;
-        return (1u << psl) <= (1u << sl) && (1u << cl) / (1u << psl) <= kSplitAcc;
+        return psl >= 1 && (1u << psl) <= (1u << sl) && (1u << cl) / (1u << psl) <= kSplitAcc;
     }
 };
 
@@ -523,7 +283,6 @@ constexpr uint32_t kWgRing = 8;    // LDS ring of published chunk ids
 constexpr uint64_t kNoChunk = 0xFFFFFFFFull;
 
 struct WgQueue {
-    unsigned int exits;    // waves of this workgroup done with the slot (MCK_SLOT_DONE)
     unsigned int slot;     // next (chunk, unit) slot of this workgroup
     unsigned int drained;  // sub-queues (counted from home) found empty
     unsigned int busy;     // 1: no slot for this launch -> static split
@@ -586,25 +345,42 @@ __device__ __noinline__ void queue_fault(uint32_t kind, uint64_t a, uint64_t b) 
 // polling one line: an iteration count had bounded nothing).  The counter is
 // read on every 16th poll only (the polls stay tight: the ring-entry wait sits
 // on the path of every unit taken) and the first read starts the clock.
-// Round 4 and before counted polls (2^24 / 2^22) instead.
+//  * Preemption: a gap of more than kGapTicks between two reads (16 polls
+//    take microseconds) means the wave was switched out -- CWSR, when other
+//    processes share the GPU -- and that time does not count, so a healthy
+//    launch resumed after a long preemption does not fail closed at once.
+//  * Abort: the launch's abort flag (kQAbort; nullptr for waits outside the
+//    queue) is read with the counter; once any wait of the launch has given
+//    up, every other one gives up at its next read, so a call meets at most
+//    one deadline however many stalls it has.
 #ifndef MCK_WAIT_TICKS
 #define MCK_WAIT_TICKS 100000000ull  // 1 s at 100 MHz
 #endif
 constexpr uint64_t kWaitTicks = MCK_WAIT_TICKS;
+constexpr uint64_t kGapTicks = 5000000ull;  // 50 ms
 struct Deadline {
-    uint64_t t0 = 0;
+    const unsigned long long *abort = nullptr;
+    uint64_t t0 = 0, last = 0;
     uint32_t polls = 0;
-    // true once this wait has lasted kWaitTicks (call once per poll)
+    __device__ explicit Deadline(const unsigned long long *abort_word = nullptr) : abort(abort_word) {}
+    // true once this wait has lasted kWaitTicks, or the launch aborted (call once per poll)
     __device__ __forceinline__ bool passed() {
         if ((++polls & 15u) != 1u) return false;
         const uint64_t now = wall_clock64();
         if (polls == 1u) {
-            t0 = now;
-            return false;
+            t0 = last = now;
+            return abort && __hip_atomic_load(abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        return now - t0 > kWaitTicks;
+        if (now - last > kGapTicks) t0 += now - last;  // switched out: not waiting time
+        last = now;
+        return now - t0 > kWaitTicks || (abort && __hip_atomic_load(abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     }
 };
+// The launch's abort flag in its bank (queue non-null), set by a wave whose wait gave up.
+__device__ __forceinline__ unsigned long long *abort_word(unsigned long long *q) { return q + kQAbort * kQStride; }
+__device__ __forceinline__ void raise_abort(unsigned long long *q) {
+    if (q) __hip_atomic_store(abort_word(q), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 #define MCK_WAIT_GUARD(dl, kind, A_, B_) \
     if ((dl).passed()) {                 \
         queue_fault(kind, A_, B_);       \
@@ -619,11 +395,11 @@ struct Deadline {
 // look-back); 1 = "stall": workgroup 3 never publishes its third chunk, so its
 // waves wait out the deadline; 2 = "scanstall": segment-scan block
 // MCHECKSUM_GPU_QFAULT_SCAN never publishes its look-back descriptor, so its
-// successors wait out theirs (nothing else is injected).
+// successors wait out theirs; 3 = "stall+scanstall": both in one call.
 __device__ unsigned int g_mck_qfault_mode;
 #endif
 
-// Steal order (MCK_STEAL_ROT=0: every thief starts at home + 1).  On since
+// Steal order: thieves of one home start at different victims.  On since
 // round 3: never slower in four one-process A/Bs over rounds 3-4 (headline
 // +0.1 to +0.2%, C4 +0.14 to +0.55%; profiles/r03/ab_steal_rot*.log,
 // profiles/r04/ab_qmask.log) -- gains inside the run-to-run band, kept because
@@ -631,22 +407,15 @@ __device__ unsigned int g_mck_qfault_mode;
 // sub-queues, run by the CPU model in tests/test_queue_model.py).  A drained-
 // state mask read before stealing (one load per fetch instead of an atomic on
 // each drained sub-queue) measured -0.1% / -0.5% and is gone.
-#ifndef MCK_STEAL_ROT
-#define MCK_STEAL_ROT 1
-#endif
 // One lane: the next global chunk id for this workgroup, or kNoChunk.
 __device__ uint64_t wg_fetch(WgQueue *L, unsigned long long *q, uint64_t nch) {
     const uint32_t home = blockIdx.x % kQSub;
     uint32_t d = lds_ld(&L->drained);
     while (d < kQSub) {
-#if MCK_STEAL_ROT
         // thieves of one home start at different victims (a rotation of the
         // other seven by workgroup), so a drained XCD's 32 workgroups do not
         // all queue on the next sub-queue's counter at the end of the batch
         const uint32_t k = d == 0 ? home : (home + 1 + (d - 1 + (blockIdx.x / kQSub) % (kQSub - 1)) % (kQSub - 1)) % kQSub;
-#else
-        const uint32_t k = (home + d) % kQSub;
-#endif
         // sub-queue k owns chunks k, k + 8, k + 16, ...: every XCD streams
         // from the same moving window of the batch (contiguous per-XCD ranges
         // -- 8 windows far apart -- measured 8% slower on the headline batch)
@@ -660,16 +429,18 @@ __device__ uint64_t wg_fetch(WgQueue *L, unsigned long long *q, uint64_t nch) {
 }
 
 // One lane: make chunk `seq` of this workgroup known in the ring.  Returns
-// false when the wait for the ring entry's readers gave up (fault counted).
-__device__ bool wg_publish(WgQueue *L, uint32_t seq, uint64_t id, uint32_t cl) {
+// false when the wait for the ring entry's readers gave up (fault counted,
+// the launch's abort flag raised).
+__device__ bool wg_publish(WgQueue *L, unsigned long long *q, uint32_t seq, uint64_t id, uint32_t cl) {
     const uint32_t r = seq % kWgRing;
     bool ok = true;
-    Deadline dl;
+    Deadline dl(abort_word(q));
     if (seq >= kWgRing)
         while (lds_ld(&L->reads[r]) != (1u << cl)) {
             __builtin_amdgcn_s_sleep(1);
             if (dl.passed()) {
                 queue_fault(1, seq, lds_ld(&L->reads[r]));
+                raise_abort(q);
                 ok = false;
                 break;
             }
@@ -692,7 +463,6 @@ __device__ bool wg_publish(WgQueue *L, uint32_t seq, uint64_t id, uint32_t cl) {
 // front of thread 0's wave's table fill (waves look for a chunk only after
 // their first unit; until the publish they wait on the ring entry).
 __device__ __attribute__((unused)) void wg_queue_reset(WgQueue *L, unsigned long long *q) {
-    L->exits = 0;
     L->slot = 0;
     L->drained = 0;
     L->busy = q == nullptr;
@@ -709,7 +479,7 @@ __device__ __attribute__((unused)) void wg_queue_start_plan(WgQueue *L, unsigned
 #pragma unroll
         for (uint32_t j = 0; j < kQBankLines; j++) atomicExch(o + j * kQStride, 0ull);
     }
-    (void)wg_publish(L, 0, wg_fetch(L, q, plan.nch), plan.cl);
+    (void)wg_publish(L, q, 0, wg_fetch(L, q, plan.nch), plan.cl);
 }
 __device__ __attribute__((unused)) void wg_queue_start(WgQueue *L, unsigned long long *q, uint64_t n) {
     if (!q) return;
@@ -725,32 +495,6 @@ __device__ __attribute__((unused)) void wg_queue_init_plan(WgQueue *L, unsigned 
     wg_queue_start_plan(L, q, plan);
 }
 
-#if MCK_SLOT_DONE
-// 64-bit store of v at p through the vector memory path to system scope (the
-// slot's completion word in host-mapped memory)
-__device__ __forceinline__ void store_system_u64(unsigned long long *p, unsigned long long v) {
-    asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1" : : "v"(p), "v"(v) : "memory");
-}
-// A wave of a slot launch is done with the slot (see "Completion" above).
-// Every slot access before this point is an atomic (returning, or the bank
-// zeroing counted by vmcnt), so once vmcnt drains the wave's part is performed.
-__device__ __forceinline__ void slot_exit(WgQueue *L, unsigned long long *q, bool l0) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (!l0) return;
-    const uint32_t waves = blockDim.x >> 6;
-    if (__hip_atomic_fetch_add(&L->exits, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP) != waves - 1) return;
-    const uint32_t g = blockIdx.x % kQSub, G = gridDim.x;
-    const unsigned long long in_group = (G - g + kQSub - 1) / kQSub, groups = G < kQSub ? G : kQSub;
-    if (atomicAdd(q + (kQExitGroup + g) * kQStride, 1ull) != in_group - 1) return;
-    if (atomicAdd(q + kQExitTop * kQStride, 1ull) != groups - 1) return;
-    // the launch's last workgroup: the slot's launch count, to the host
-    const uintptr_t slot = reinterpret_cast<uintptr_t>(q) & ~(uintptr_t)(2 * kQBankBytes - 1);
-    unsigned long long *sq = reinterpret_cast<unsigned long long *>(slot);
-    const unsigned long long n = atomicAdd(sq + kQLaunchLine * kQStride, 1ull) + 1ull;
-    const uintptr_t idx = (slot - reinterpret_cast<uintptr_t>(g_mck_qbase)) / (2 * kQBankBytes);
-    if (g_mck_slot_done) store_system_u64(g_mck_slot_done + idx, n);
-}
-#endif
 
 template <typename T>
 __device__ __forceinline__ T wave_max(T v) {
@@ -797,14 +541,11 @@ __device__ __forceinline__ bool for_each_unit(WgQueue *L, unsigned long long *qu
         const uint64_t q0 = FIRST ? first_static_units(n, nw) : 0;
         uint64_t su = FIRST ? (uint64_t)wave + nw : wave;  // static cursor (busy slot)
         const bool l0 = (threadIdx.x & 63u) == 0;
-#ifndef MCK_QLEAD_DIV
-#define MCK_QLEAD_DIV 4
-#endif
         const Plan plan = [&] {
             if constexpr (std::is_same_v<Plan, ChunkPlan>) return given ? *given : ChunkPlan(n - q0);
             else return *given;
         }();
-        const uint32_t cl = plan.cl, cu = 1u << cl, lead = cu > MCK_QLEAD_DIV ? cu / MCK_QLEAD_DIV : 1;
+        const uint32_t cl = plan.cl, cu = 1u << cl, lead = cu > 4 ? cu / 4 : 1;
         const uint64_t nch = plan.nch;
 #if MCK_TRACE
         unsigned long long qs_n = 0, qs_sum = 0, qs_max = 0, qs_wait = 0, qs_busy = 0, qs_units = 0;
@@ -833,7 +574,7 @@ __device__ __forceinline__ bool for_each_unit(WgQueue *L, unsigned long long *qu
                 if (l0) {
                     t = atomicAdd(&L->slot, 1u);
                     const uint32_t seq = t >> cl, r = seq % kWgRing;
-                    Deadline dl;
+                    Deadline dl(abort_word(queue));
 #if MCK_TRACE
                     const unsigned long long w0 = wall_clock64();
                     unsigned long long f0 = 0;
@@ -846,6 +587,7 @@ __device__ __forceinline__ bool for_each_unit(WgQueue *L, unsigned long long *qu
                     qs_wait += wall_clock64() - w0;
 #endif
                     if ((e >> 32) != seq) {  // gave up (fault counted)
+                        raise_abort(queue);
                         e = kNoChunk;
                         flt = 1;
                     }
@@ -862,7 +604,7 @@ __device__ __forceinline__ bool for_each_unit(WgQueue *L, unsigned long long *qu
                         // publishes its third chunk (no chunk is lost: the
                         // other workgroups take every unit), so each of its
                         // waves waits out the deadline on that ring entry
-                        const bool stall = g_mck_qfault_mode == 1u && blockIdx.x == 3 && seq == 1;
+                        const bool stall = (g_mck_qfault_mode & 1u) && blockIdx.x == 3 && seq == 1;
 #else
                         constexpr bool stall = false;
 #endif
@@ -874,7 +616,7 @@ __device__ __forceinline__ bool for_each_unit(WgQueue *L, unsigned long long *qu
                         qs_sum += df;
                         qs_max = df > qs_max ? df : qs_max;
 #endif
-                        if (!stall && !wg_publish(L, seq + 1, nid, cl)) flt = 1;
+                        if (!stall && !wg_publish(L, queue, seq + 1, nid, cl)) flt = 1;
                     }
 #if MCK_QFAULT_TEST
                     // injected give-up: workgroup 3 drops the first unit of its
@@ -930,9 +672,6 @@ __device__ __forceinline__ bool for_each_unit(WgQueue *L, unsigned long long *qu
         uint32_t first = 0;
         if (l0 && flt) first = atomicCAS(queue + kQFault * kQStride, 0ull, 1ull) == 0ull;
         (void)nw;
-#if MCK_SLOT_DONE
-        slot_exit(L, queue, l0);
-#endif
         return __builtin_amdgcn_readfirstlane(first) != 0;
     } else {
         for (uint64_t u = FIRST ? (uint64_t)wave + nw : wave; u < n; u += nw) {
@@ -994,13 +733,9 @@ __device__ __forceinline__ uint64_t lds64(const uint8_t *lds, uint32_t a) {
 // a ^ b ^ c in one VALU op: gfx950's v_bitop3_b32 with truth table 0x96
 // (there is no v_xor3_b32 on CDNA; hipcc does not form bitop3 from ^ chains).
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
-#if MCK_BITOP3
     uint32_t r;
     asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
     return r;
-#else
-    return a ^ b ^ c;
-#endif
 }
 
 // Z^(16G)(x): main[p][byte_p(x)], tables p=0,1 in LDS region 0 (lc0), p=2,3
@@ -1053,20 +788,17 @@ __device__ __forceinline__ uint32_t oplv32(Tab32<false> tab, uint32_t l, uint32_
 }
 
 // XOR_q Z^(-4q)(S_q) in the lane, then over the G lanes of the group.  For
-// G = 64 on the throughput layout (MCK_LV32): lane l = 8a + b applies
+// G = 64 on the throughput layout: lane l = 8a + b applies
 // Z^(-16b), the 8 lanes of each a XOR-reduce (shuffles only), the groups
 // apply Z^(-128a) and XOR-reduce -- two table operators on the lane's path
 // instead of six butterfly levels of one each.
-#ifndef MCK_LV32
-#define MCK_LV32 1
-#endif
 template <int LOG2G, class TAB>
 __device__ __forceinline__ uint32_t combine32(TAB lds, uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3,
                                               uint32_t gl) {
     uint32_t x = s0 ^ op32(lds, 0, s1);
     const uint32_t y = s2 ^ op32(lds, 0, s3);
     x ^= op32(lds, 1, y);
-    if constexpr (MCK_LV32 && LOG2G == 6 && std::is_same<TAB, Tab32<false>>::value) {
+    if constexpr (LOG2G == 6 && std::is_same<TAB, Tab32<false>>::value) {
         x = oplv32(lds, 0, gl & 7u, x);
         x ^= __shfl_xor(x, 1, 64);
         x ^= __shfl_xor(x, 2, 64);
@@ -1154,18 +886,6 @@ __device__ void fill_lds32(uint8_t *lds, const crc32_gpu_pack_t *pk, F &&issue =
 //
 // Aligned fixed-size payload: base 16-B aligned, len = K * 16G, no masking,
 // no pad bytes (tail op is the identity and is skipped).
-#ifndef MCK_ALIGNED32_V2
-#define MCK_ALIGNED32_V2 1
-#endif
-#ifndef MCK_LA32
-#define MCK_LA32 1
-#endif
-#ifndef MCK_PREFETCH32
-#define MCK_PREFETCH32 1
-#endif
-#ifndef MCK_PREFETCH32_LIGHT
-#define MCK_PREFETCH32_LIGHT 0
-#endif
 // Global-address-space views: loads through them are global_load (never
 // flat_load, which would also count against lgkmcnt and make every LDS wait
 // wait for HBM), and a wave-uniform base in SGPRs gives the saddr form.
@@ -1184,7 +904,6 @@ __device__ __forceinline__ uint4 ldg16(gbyte_t p) {
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
-#if MCK_ALIGNED32_V2
 // Aligned step loop without per-step tests: K is a multiple of kRing and
 // >= kRing (launch_fixed's aligned test), so every load of the steady loop is
 // in range and the last kRing steps run without loads.  The load pointer
@@ -1216,7 +935,6 @@ __device__ __forceinline__ uint32_t payload32_aligned(TAB lds, const uint8_t *p,
     if (!loaded) ring32_load<LOG2G, NT>(ring, p, gl);
     lb += R * S;
     uint32_t x0 = gl == 0 ? init : 0u, x1 = 0, x2 = 0, x3 = 0;
-#if MCK_LA32
     // look-ahead: y holds state ^ (data of the step about to run), and the
     // next step's data word rides in the table-XOR tree (2 v_bitop3, no XOR)
     uint32_t y0 = x0 ^ ring[0].x, y1 = ring[0].y, y2 = ring[0].z, y3 = ring[0].w;
@@ -1245,57 +963,7 @@ __device__ __forceinline__ uint32_t payload32_aligned(TAB lds, const uint8_t *p,
     x2 = f32s(lds, y2, lc0, lc1);
     x3 = f32s(lds, y3, lc0, lc1);
     return combine32<LOG2G>(lds, x0, x1, x2, x3, gl);
-#else
-    for (uint32_t k = R; k < K; k += R) {
-#pragma unroll
-        for (uint32_t u = 0; u < R; u++) {
-            const uint32_t y0 = x0 ^ ring[u].x, y1 = x1 ^ ring[u].y, y2 = x2 ^ ring[u].z, y3 = x3 ^ ring[u].w;
-            ring[u] = ldg16<NT>(lb + (lo + u * S));
-            x0 = f32s(lds, y0, lc0, lc1);
-            x1 = f32s(lds, y1, lc0, lc1);
-            x2 = f32s(lds, y2, lc0, lc1);
-            x3 = f32s(lds, y3, lc0, lc1);
-        }
-        lb += R * S;
-    }
-#endif
-#pragma unroll
-    for (uint32_t u = 0; u < R; u++) {
-        x0 = f32s(lds, x0 ^ ring[u].x, lc0, lc1);
-        x1 = f32s(lds, x1 ^ ring[u].y, lc0, lc1);
-        x2 = f32s(lds, x2 ^ ring[u].z, lc0, lc1);
-        x3 = f32s(lds, x3 ^ ring[u].w, lc0, lc1);
-    }
-    return combine32<LOG2G>(lds, x0, x1, x2, x3, gl);
 }
-#else
-template <int LOG2G, bool NT, class TAB>
-__device__ __forceinline__ uint32_t payload32_aligned(TAB lds, const uint8_t *p, uint64_t K, uint32_t gl,
-                                                      uint32_t lc0, uint32_t lc1, uint32_t init,
-                                                      uint4 (&)[kRing], bool) {
-    constexpr int G = 1 << LOG2G;
-    const uint4 *src = reinterpret_cast<const uint4 *>(p) + gl;
-    uint4 ring[kRing];
-#pragma unroll
-    for (int u = 0; u < kRing; u++) ring[u] = (uint64_t)u < K ? ld16<NT>(src + (uint64_t)u * G) : make_uint4(0, 0, 0, 0);
-    uint32_t x0 = gl == 0 ? init : 0u, x1 = 0, x2 = 0, x3 = 0;
-    for (uint64_t k = 0; k < K; k += kRing) {
-#pragma unroll
-        for (int u = 0; u < kRing; u++) {
-            const uint4 v = ring[u];
-            const uint64_t kn = k + u + kRing;
-            if (kn < K) ring[u] = ld16<NT>(src + kn * G);
-            if (k + u < K) {
-                x0 = f32s(lds, x0 ^ v.x, lc0, lc1);
-                x1 = f32s(lds, x1 ^ v.y, lc0, lc1);
-                x2 = f32s(lds, x2 ^ v.z, lc0, lc1);
-                x3 = f32s(lds, x3 ^ v.w, lc0, lc1);
-            }
-        }
-    }
-    return combine32<LOG2G>(lds, x0, x1, x2, x3, gl);
-}
-#endif
 template <int LOG2G, bool NT, class TAB>
 __device__ __forceinline__ uint32_t payload32_aligned(TAB lds, const uint8_t *p, uint64_t K, uint32_t gl,
                                                       uint32_t lc0, uint32_t lc1, uint32_t init) {
@@ -1369,17 +1037,14 @@ __device__ __forceinline__ uint32_t payload32_generic(TAB lds, const crc32_gpu_p
 
 // Step grid of the one-payload-per-wave loops (payload32_g64 / payload64_g64):
 // the window of 1 KiB steps ENDS on a 128-B line boundary past the payload
-// (MCK_ALIGN128; 16 B before round 3), so every step reads exactly 8 whole
+// (16 B before round 3), so every step reads exactly 8 whole
 // lines.  With non-temporal loads a line that two steps straddle is fetched
 // twice: on C4's byte-packed payloads that was 1.7% of extra HBM requests
 // (TCC_EA0_RDREQ: 6.83e7 vs 6.74e7 with NT off, profiles/r03/tcc_c4_nt*.txt;
 // NT off costs 11%).  Reads stay inside the last byte's 128-B line, hence
 // its page.  The up-to-127 pad bytes are removed by Z^-t, t = 16q + r: the
 // tail table Z^-r and the butterfly operators Z^-(16*2^k) for the bits of q.
-#ifndef MCK_ALIGN128
-#define MCK_ALIGN128 1
-#endif
-constexpr uint64_t kGridAlign = MCK_ALIGN128 ? 128 : 16;
+constexpr uint64_t kGridAlign = 128;
 
 template <class TAB>
 __device__ __forceinline__ uint32_t tail32(TAB lds, uint32_t t, uint32_t x) {
@@ -1544,9 +1209,6 @@ __global__ __launch_bounds__(kBlk32<LIGHT>, 1) void crc32c_batch_kernel(BatchArg
     const uint64_t units = MODE == kOffsets ? a.count : (a.count + PPW - 1) / PPW;
     __shared__ WgQueue wgq;
     constexpr bool DYN = dyn_policy(32, MODE, NT, LIGHT);
-#if defined(MCK_EMPTY) && MCK_EMPTY == 2
-    if (!DYN) return;  // diagnostic: launch cost alone
-#endif
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t gl = lane & ((1u << LOG2G) - 1u), grp = lane >> LOG2G;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
@@ -1554,22 +1216,16 @@ __global__ __launch_bounds__(kBlk32<LIGHT>, 1) void crc32c_batch_kernel(BatchArg
     // Aligned batches on the static split (C2): the loads of the wave's first
     // payload go out inside the LDS table fill, so their HBM round trip
     // overlaps the fill's.  The queue path (the headline) keeps its first unit
-    // dynamic: a static first unit there (MCK_PREFETCH32 >= 2, for_each_unit
-    // <DYN, true>) measured 1% slower; the
-    // light layout gains nothing from it (MCK_PREFETCH32_LIGHT).
-    constexpr bool PRE = MODE == kFixedAligned && (!LIGHT || MCK_PREFETCH32_LIGHT) && MCK_ALIGNED32_V2 &&
-                         (DYN ? MCK_PREFETCH32 >= 2 : MCK_PREFETCH32 >= 1);
-    constexpr bool LATE_START = PRE && DYN && MCK_PREFETCH32 == 2;
+    // dynamic: a static first unit there measured 1% slower (round 3); the
+    // light layout gained nothing from it.
+    constexpr bool PRE = MODE == kFixedAligned && !LIGHT && !DYN;
     // model words read once, ahead of any store (scalar loads; read after the
     // barrier they became a vector load per payload whose wait, merged with
     // the ring's at the prefetch branch, cost a vmcnt(0) per payload)
     const uint32_t init = pk->init, xorout = pk->xorout;
     uint4 ring0[kRing];
     const bool pre = PRE && wave < units;
-    if (DYN && threadIdx.x == 0) {
-        if (LATE_START) wg_queue_reset(&wgq, a.queue);
-        else wg_queue_init(&wgq, a.queue, PRE ? units - first_static_units(units, nw) : units);
-    }
+    if (DYN && threadIdx.x == 0) wg_queue_init(&wgq, a.queue, units);
     fill_lds32<LIGHT, kBlk32<LIGHT>>(lds_raw, pk, [&] {
         // Throughput layout: unconditional (a wave without a first unit reads
         // the last payload's first steps) -- loads under a branch leave the
@@ -1584,10 +1240,6 @@ __global__ __launch_bounds__(kBlk32<LIGHT>, 1) void crc32c_batch_kernel(BatchArg
         }
     });
     __syncthreads();
-    if (LATE_START && threadIdx.x == 0) wg_queue_start(&wgq, a.queue, units - first_static_units(units, nw));
-#if defined(MCK_EMPTY) && MCK_EMPTY == 1
-    if (!DYN) return;  // diagnostic: launch + LDS table fill
-#endif
     MCK_STAMP(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6), 1);
     const Tab32<LIGHT> lds{lds_raw};
 
@@ -1688,109 +1340,16 @@ __device__ __forceinline__ uint64_t xor17(const uint64_t *r, uint64_t extra) {
     return xor3_64(xor3_64(r[15], extra, a), xor3_64(b, c, d), e);
 }
 
-#ifndef MCK_SDWA64
-#define MCK_SDWA64 1
-#endif
-
-// Per-lane lookup address registers of f64x.  With SDWA (gfx9 sub-dword
-// operands) one v_and_b32_sdwa both extracts a nibble of byte b and places it:
-// the high nibble as (byte & 0xF0) -- its own address -- and the low nibble
-// into byte 1 of a persistent register whose byte 0 holds the lane copy offset
-// (dst_unused:UNUSED_PRESERVE keeps it), so a lookup costs one VALU op and no
-// separate masking.
+// Per-lane lookup address registers of f64x: the lane-copy offset in byte 0
+// of four persistent registers, whose byte 1 the pair index is written into
+// by one v_and_b32_sdwa each (dst_unused:UNUSED_PRESERVE keeps byte 0), so a
+// replicated lookup costs one VALU op and no separate masking.
 struct Lane64 {
     uint32_t lc;
     uint32_t al[4];
 };
 __device__ __forceinline__ Lane64 lane64(uint32_t lc) { return Lane64{lc, {lc, lc, lc, lc}}; }
-// kFold11: the lane-copy registers of the four 7-bit tables and the 6-bit
-// one, each with its 64 KiB region in byte 2
-struct Lane64F11 {
-    uint32_t a7[4];
-    uint32_t a6;
-};
-// kFold12W: the lane copy (plain and with region 1), the three SDWA pair
-// registers (region 1) and the masks, all in VGPRs (an SGPR operand costs a
-// VALU op ~1 cycle more)
-struct Lane64W {
-    uint32_t lc, lcr, al0, al2, al3;
-    uint32_t m8, mF800, m3F00, m07;
-};
-template <int FL>
-using LaneT = std::conditional_t<FL == kFold11, Lane64F11, std::conditional_t<FL == kFold12W, Lane64W, Lane64>>;
-__device__ __forceinline__ uint32_t vmov(uint32_t m) {
-    uint32_t r;
-    asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "s"(m));
-    return r;
-}
-template <int FL>
-__device__ __forceinline__ LaneT<FL> lane_regs(uint32_t lc) {
-    if constexpr (FL == kFold11) {
-        return Lane64F11{{lc, lc, lc | 0x10000u, lc | 0x10000u}, lc | 0x20000u};
-    } else if constexpr (FL == kFold12W) {
-        const uint32_t r1 = lc | 0x10000u;
-        return Lane64W{lc, r1, r1, r1, r1, vmov(0xF8u), vmov(0xF800u), vmov(0x3F00u), vmov(0x07070707u)};
-    } else {
-        return lane64(lc);
-    }
-}
 
-#define MCK_SDWA_HI(B)                                                                              \
-    __device__ __forceinline__ uint32_t sdwa_hi##B(uint32_t x) {                                    \
-        uint32_t r;                                                                                 \
-        asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD "         \
-            "src1_sel:BYTE_" #B : "=v"(r) : "s"(0xF0u), "v"(x));                                    \
-        return r;                                                                                   \
-    }                                                                                               \
-    __device__ __forceinline__ void sdwa_lo##B(uint32_t &a, uint32_t x) {                           \
-        asm("v_and_b32_sdwa %0, %1, %2 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD "   \
-            "src1_sel:BYTE_" #B : "+v"(a) : "s"(0x0Fu), "v"(x));                                    \
-    }
-MCK_SDWA_HI(0)
-MCK_SDWA_HI(1)
-MCK_SDWA_HI(2)
-MCK_SDWA_HI(3)
-#undef MCK_SDWA_HI
-
-template <int B>
-__device__ __forceinline__ uint32_t sdwa_hi(uint32_t x) {
-    if constexpr (B == 0) return sdwa_hi0(x);
-    else if constexpr (B == 1) return sdwa_hi1(x);
-    else if constexpr (B == 2) return sdwa_hi2(x);
-    else return sdwa_hi3(x);
-}
-template <int B>
-__device__ __forceinline__ void sdwa_lo(uint32_t &a, uint32_t x) {
-    if constexpr (B == 0) sdwa_lo0(a, x);
-    else if constexpr (B == 1) sdwa_lo1(a, x);
-    else if constexpr (B == 2) sdwa_lo2(a, x);
-    else sdwa_lo3(a, x);
-}
-
-#if !MCK_CRC64_P6
-template <int B>
-__device__ __forceinline__ void f64x_byte(const uint8_t *lds, uint32_t xl, uint32_t xh, Lane64 &ln, uint64_t *r) {
-#if MCK_SDWA64
-    sdwa_lo<B>(ln.al[B], xl);
-    r[4 * B + 0] = lds64(lds, ln.al[B] + B * 4096);
-    r[4 * B + 1] = lds64(lds, sdwa_hi<B>(xl) + kL64Hi + B * 256);
-    sdwa_lo<B>(ln.al[B], xh);
-    r[4 * B + 2] = lds64(lds, ln.al[B] + (B + 4) * 4096);
-    r[4 * B + 3] = lds64(lds, sdwa_hi<B>(xh) + kL64Hi + B * 256 + 8);
-#else
-    const uint32_t sl = 0x0C0C0400u | ((uint32_t)B << 8);  // byte B -> address byte 1, lane byte -> 0
-    const uint32_t sh = 0x0C0C0C04u | (uint32_t)B;         // byte B -> address byte 0
-    const uint32_t l0 = xl & 0x0F0F0F0Fu, h0 = xl & 0xF0F0F0F0u;
-    const uint32_t l1 = xh & 0x0F0F0F0Fu, h1 = xh & 0xF0F0F0F0u;
-    r[4 * B + 0] = lds64(lds, __builtin_amdgcn_perm(l0, ln.lc, sl) + B * 4096);
-    r[4 * B + 1] = lds64(lds, __builtin_amdgcn_perm(h0, h0, sh) + kL64Hi + B * 256);
-    r[4 * B + 2] = lds64(lds, __builtin_amdgcn_perm(l1, ln.lc, sl) + (B + 4) * 4096);
-    r[4 * B + 3] = lds64(lds, __builtin_amdgcn_perm(h1, h1, sh) + kL64Hi + B * 256 + 8);
-#endif
-}
-#endif
-
-#if MCK_CRC64_P6
 // (byte B of x) & 0xF8: a 5-bit field scaled by 8, its own f5 address;
 // (byte B of t) & 0x3F into byte 1 of the lane-copy register a.
 #define MCK_SDWA_P6(B)                                                                              \
@@ -1816,67 +1375,30 @@ MCK_SDWA_P6(3)
 // four pair indexes: round 1 paired bytes (2i, 2i+1) within a half, which took
 // a shift and a bit-select per half (28 -> 26 VALU ops per 8-byte word on a
 // VALU-bound loop).  The C form (x & m) | (y & ~m) compiled to v_and +
-// v_and_or: one op more.
-#ifndef MCK_BFI64
-#define MCK_BFI64 1
-#endif
-// Round 5 (tools/valu_probe.hip, profiles/r05/valu_probe.txt): on gfx950 a
-// wave64 v_bitop3_b32 / v_and_b32 / v_xor_b32 with VGPR operands issues in
-// ~1.8 shader cycles per SIMD (4 waves/SIMD), v_bfi_b32, v_perm_b32, every
-// SDWA form and any VALU op with an SGPR operand in ~2.8.  MCK_CHEAP64=1: the
-// bit-select as a v_bitop3 (S0 ? S1 : S2 = 0xCA) with its mask in a VGPR, and
-// byte 0's f5 address as a VOP2 AND with a VGPR mask, instead of v_bfi_b32 and
-// an SDWA AND with the mask in SGPRs.
-#ifndef MCK_CHEAP64
-#define MCK_CHEAP64 0
-#endif
-__device__ __forceinline__ uint32_t vmask(uint32_t m) {
-    uint32_t r;
-    asm("v_mov_b32 %0, %1" : "=v"(r) : "s"(m));  // loop-invariant: hoisted by the compiler
-    return r;
-}
-__device__ __forceinline__ uint32_t and_v(uint32_t x, uint32_t mv) {
-    uint32_t r;
-    asm("v_and_b32 %0, %1, %2" : "=v"(r) : "v"(mv), "v"(x));
-    return r;
-}
+// v_and_or: one op more.  (Round 5: the bit-select as a v_bitop3 with its mask
+// in a VGPR, which the probe issues faster, measured +-0 in the loop.)
 __device__ __forceinline__ uint32_t gather6(uint32_t xl, uint32_t xh) {
-#if MCK_BFI64 && MCK_CHEAP64
-    uint32_t r;
-    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xca" : "=v"(r) : "v"(vmask(0x07070707u)), "v"(xl), "v"(xh << 3));
-    return r;
-#elif MCK_BFI64
     uint32_t r;
     asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(0x07070707u), "v"(xl), "v"(xh << 3));
     return r;
-#else
-    return (xl & 0x07070707u) | ((xh << 3) & ~0x07070707u);
-#endif
 }
 __device__ __forceinline__ uint64_t xor13(const uint64_t *r, uint64_t extra) {
     const uint64_t a = xor3_64(r[0], r[1], r[2]), b = xor3_64(r[3], r[4], r[5]), c = xor3_64(r[6], r[7], r[8]);
     return xor3_64(a, b, xor3_64(c, xor3_64(r[9], r[10], r[11]), extra));
 }
-// Z^(16G)(x) ^ next from the 12 tables f5/f6 (LDS map above).
+// Z^(16G)(x) ^ next from the 12 tables f5/f6 (LDS map above): 12 address
+// ops, 2 for the gather, 12 v_bitop3 for the XOR tree (the next data word
+// rides in its 13th input).
 __device__ __forceinline__ uint64_t f64x(const uint8_t *lds, uint64_t x, uint64_t next, Lane64 &ln) {
     const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
     // byte i of t: bits 0..2 of bytes i and i + 4 of the word (bit-select)
     const uint32_t t = gather6(xl, xh);
     uint64_t r[12];
-#if MCK_CHEAP64
-    const uint32_t m8 = vmask(0xF8u);
-    r[0] = lds64(lds, and_v(xl, m8) + kL64P5 + 0 * 256);
-#else
     r[0] = lds64(lds, sdwa_f8_0(xl) + kL64P5 + 0 * 256);
-#endif
     r[1] = lds64(lds, sdwa_f8_1(xl) + kL64P5 + 1 * 256);
     r[2] = lds64(lds, sdwa_f8_2(xl) + kL64P5 + 2 * 256);
     r[3] = lds64(lds, sdwa_f8_3(xl) + kL64P5 + 3 * 256);
-#if MCK_CHEAP64
-    r[4] = lds64(lds, and_v(xh, m8) + kL64P5 + 4 * 256);
-#else
     r[4] = lds64(lds, sdwa_f8_0(xh) + kL64P5 + 4 * 256);
-#endif
     r[5] = lds64(lds, sdwa_f8_1(xh) + kL64P5 + 5 * 256);
     r[6] = lds64(lds, sdwa_f8_2(xh) + kL64P5 + 6 * 256);
     r[7] = lds64(lds, sdwa_f8_3(xh) + kL64P5 + 7 * 256);
@@ -1890,111 +1412,6 @@ __device__ __forceinline__ uint64_t f64x(const uint8_t *lds, uint64_t x, uint64_
     r[11] = lds64(lds, ln.al[3] + kL64P6 + 3 * 16384);
     return xor13(r, next);
 }
-#else
-// Z^(16G)(x) ^ next from the 16 nibble tables (LDS map above): one VALU op per
-// lookup to form its address, 8 v_bitop3 per 32-bit half for the XOR tree.
-__device__ __forceinline__ uint64_t f64x(const uint8_t *lds, uint64_t x, uint64_t next, Lane64 &ln) {
-    const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
-    uint64_t r[16];
-    f64x_byte<0>(lds, xl, xh, ln, r);
-    f64x_byte<1>(lds, xl, xh, ln, r);
-    f64x_byte<2>(lds, xl, xh, ln, r);
-    f64x_byte<3>(lds, xl, xh, ln, r);
-    return xor17(r, next);
-}
-#endif
-
-#if MCK_CRC64_P6
-// (x & m) | c in one v_bitop3 (truth table 0xEA), every operand a VGPR
-__device__ __forceinline__ uint32_t andor3(uint32_t x, uint32_t m, uint32_t c) {
-    uint32_t r;
-    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xea" : "=v"(r) : "v"(x), "v"(m), "v"(c));
-    return r;
-}
-// s ? a : b bitwise in one v_bitop3 (0xCA), every operand a VGPR
-__device__ __forceinline__ uint32_t sel3(uint32_t s, uint32_t a, uint32_t b) {
-    uint32_t r;
-    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xca" : "=v"(r) : "v"(s), "v"(a), "v"(b));
-    return r;
-}
-// Z^(16G)(x) ^ next, the 12 lookups of the pack's f5 / f6 tables in the
-// kFold12W map (above): 9 address ops at ~1.8 cycles + 3 SDWA instead of 12 SDWA.
-__device__ __forceinline__ uint64_t f64x(const uint8_t *lds, uint64_t x, uint64_t next, Lane64W &ln) {
-    const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
-    const uint32_t yl = xl >> 16, yh = xh >> 16;
-    uint64_t r[12];
-    r[0] = lds64(lds, and_v(xl, ln.m8) + kWUnrep + 0 * 256);
-    r[1] = lds64(lds, andor3(xl, ln.mF800, ln.lc) + 0 * 256);
-    r[2] = lds64(lds, and_v(yl, ln.m8) + kWUnrep + 1 * 256);
-    r[3] = lds64(lds, andor3(yl, ln.mF800, ln.lc) + 1 * 256);
-    r[4] = lds64(lds, and_v(xh, ln.m8) + kWUnrep + 2 * 256);
-    r[5] = lds64(lds, andor3(xh, ln.mF800, ln.lc) + 2 * 256);
-    r[6] = lds64(lds, and_v(yh, ln.m8) + kWUnrep + 3 * 256);
-    r[7] = lds64(lds, andor3(yh, ln.mF800, ln.lc) + 3 * 256);
-    const uint32_t t = sel3(ln.m07, xl, xh << 3);
-    sdwa_p6_0(ln.al0, t);
-    r[8] = lds64(lds, ln.al0 + (kWF6 - 65536) + 0 * 16384);
-    r[9] = lds64(lds, andor3(t, ln.m3F00, ln.lcr) + (kWF6 - 65536) + 1 * 16384);
-    sdwa_p6_2(ln.al2, t);
-    r[10] = lds64(lds, ln.al2 + (kWF6 - 65536) + 2 * 16384);
-    sdwa_p6_3(ln.al3, t);
-    r[11] = lds64(lds, ln.al3 + (kWF6 - 65536) + 3 * 16384);
-    return xor13(r, next);
-}
-// (byte B of x) & 0x7F into byte 1 of the lane-copy register a (7-bit index).
-#define MCK_SDWA_P7(B)                                                                              \
-    __device__ __forceinline__ void sdwa_p7_##B(uint32_t &a, uint32_t x) {                          \
-        asm("v_and_b32_sdwa %0, %1, %2 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD "   \
-            "src1_sel:BYTE_" #B : "+v"(a) : "s"(0x7Fu), "v"(x));                                    \
-    }
-MCK_SDWA_P7(0)
-MCK_SDWA_P7(1)
-MCK_SDWA_P7(2)
-MCK_SDWA_P7(3)
-#undef MCK_SDWA_P7
-__device__ __forceinline__ uint32_t bfi32(uint32_t mask, uint32_t a, uint32_t b) {
-    uint32_t r;
-    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(mask), "v"(a), "v"(b));
-    return r;
-}
-__device__ __forceinline__ uint64_t xor12(const uint64_t *r, uint64_t extra) {
-    const uint64_t a = xor3_64(r[0], r[1], r[2]), b = xor3_64(r[3], r[4], r[5]), c = xor3_64(r[6], r[7], r[8]);
-    return xor3_64(a, b, c) ^ xor3_64(r[9], r[10], extra);
-}
-// Z^(16G)(x) ^ next in 11 lookups (kFold11 map above; the index formation is
-// restated in tests/native/kernel_emulator.cpp and checked there against the
-// nibble fold):
-//   f5[j]   bits 3..7 of byte j, j < 6          (byte & 0xF8: its own address)
-//   f7[0/1] bits 0..6 of byte 6 / 7
-//   t  = bfi(0x07070707, xl, xh << 3)           byte i: bits 0..2 of bytes i, i+4
-//   t2 = bfi(0x3F3F, t, xh >> 17)               + bit 7 of byte 6 / 7 at bit 6
-//   f7[2/3] byte 0 / 1 of t2 (7 bits)
-//   t3 = bfi(0x07070707, xl, xl >> 5)           byte 2: bits 0..2 of bytes 2, 3
-//   f6b     byte 2 of t3 (6 bits)
-__device__ __forceinline__ uint64_t f64x(const uint8_t *lds, uint64_t x, uint64_t next, Lane64F11 &ln) {
-    const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
-    uint64_t r[11];
-    r[0] = lds64(lds, sdwa_f8_0(xl) + kF11F5 + 0 * 256);
-    r[1] = lds64(lds, sdwa_f8_1(xl) + kF11F5 + 1 * 256);
-    r[2] = lds64(lds, sdwa_f8_2(xl) + kF11F5 + 2 * 256);
-    r[3] = lds64(lds, sdwa_f8_3(xl) + kF11F5 + 3 * 256);
-    r[4] = lds64(lds, sdwa_f8_0(xh) + kF11F5 + 4 * 256);
-    r[5] = lds64(lds, sdwa_f8_1(xh) + kF11F5 + 5 * 256);
-    sdwa_p7_2(ln.a7[0], xh);
-    r[6] = lds64(lds, ln.a7[0] + kF11F7a);
-    sdwa_p7_3(ln.a7[1], xh);
-    r[7] = lds64(lds, ln.a7[1] + kF11F7a + 32768);
-    const uint32_t t2 = bfi32(0x3F3Fu, gather6(xl, xh), xh >> 17);
-    sdwa_p7_0(ln.a7[2], t2);
-    r[8] = lds64(lds, ln.a7[2] + (kF11F7c - 65536));
-    sdwa_p7_1(ln.a7[3], t2);
-    r[9] = lds64(lds, ln.a7[3] + (kF11F7c - 65536 + 32768));
-    const uint32_t t3 = bfi32(0x07070707u, xl, xl >> 5);
-    sdwa_p6_2(ln.a6, t3);
-    r[10] = lds64(lds, ln.a6 + (kF11F6 - 131072));
-    return xor12(r, next);
-}
-#endif
 
 template <bool OG>
 __device__ __forceinline__ uint64_t op64(const uint8_t *lds, const crc64_gpu_pack_t *pk, uint32_t o, uint64_t x) {
@@ -2035,70 +1452,16 @@ __device__ __forceinline__ uint64_t combine64(const uint8_t *lds, const crc64_gp
     return x;
 }
 
-template <int BLOCK, int OM, int FL = kFold12>
+template <int BLOCK, int OM>
 __device__ void fill_lds64(uint8_t *lds, const crc64_gpu_pack_t *pk) {
     uint64_t *l = reinterpret_cast<uint64_t *>(lds);
     uint4 *l4 = reinterpret_cast<uint4 *>(lds);
-    if constexpr (FL == kFold12W) {
-        static_assert(OM != kOpsLds, "the wide-row map holds the butterfly operators only");
-        // odd-byte f5 tables: entry v of slot k (f5[2k + 1]) at v * 2048 + k * 256, 32 copies
-        for (uint32_t q = threadIdx.x; q < 4u * 32u * 16u; q += BLOCK) {
-            const uint32_t k = q >> 9, v = (q >> 4) & 31u;
-            const uint64_t e = pk->f5[2 * k + 1][v];
-            l4[v * 128u + k * 16u + (q & 15u)] = make_uint4((uint32_t)e, (uint32_t)(e >> 32), (uint32_t)e, (uint32_t)(e >> 32));
-        }
-        for (uint32_t d = threadIdx.x; d < 4u * 32u; d += BLOCK) l[kWUnrep / 8 + d] = pk->f5[2 * (d >> 5)][d & 31u];
-        // f6: entry v of table i at kWF6 + i * 16 KiB + v * 256 B, 32 copies
-        for (uint32_t q = threadIdx.x; q < 4096u; q += BLOCK) {
-            const uint64_t v = pk->f6[q >> 10][(q >> 4) & 63u];
-            l4[kWF6 / 16 + q] = make_uint4((uint32_t)v, (uint32_t)(v >> 32), (uint32_t)v, (uint32_t)(v >> 32));
-        }
-        if constexpr (OM == kOpsMix) {  // ops 1..6 at kL64Main
-            const uint4 *ops = reinterpret_cast<const uint4 *>(&pk->ops[1][0][0]);
-            for (uint32_t q = threadIdx.x; q < 6u * 128u; q += BLOCK) l4[kL64Main / 16 + q] = ops[q];
-        }
-        return;
-    }
-    if constexpr (FL == kFold11) {
-        static_assert(OM != kOpsLds, "the 11-lookup map holds the butterfly operators only");
-        // f7: entry v of table i at region_i + v*256 B, 32 copies (two per 16-B write)
-        for (uint32_t q = threadIdx.x; q < 4u * 128u * 16u; q += BLOCK) {
-            const uint32_t i = q >> 11, v = (q >> 4) & 127u;
-            const uint64_t e = pk->f7[i][v];
-            const uint32_t base = i < 2 ? kF11F7a + i * 32768u : kF11F7c + (i - 2) * 32768u;
-            l4[(base >> 4) + (v << 4) + (q & 15u)] = make_uint4((uint32_t)e, (uint32_t)(e >> 32), (uint32_t)e, (uint32_t)(e >> 32));
-        }
-        for (uint32_t q = threadIdx.x; q < 64u * 16u; q += BLOCK) {
-            const uint64_t e = pk->f6b[q >> 4];
-            l4[kF11F6 / 16 + q] = make_uint4((uint32_t)e, (uint32_t)(e >> 32), (uint32_t)e, (uint32_t)(e >> 32));
-        }
-        for (uint32_t d = threadIdx.x; d < 6u * 32u; d += BLOCK) l[kF11F5 / 8 + d] = pk->f5[d >> 5][d & 31u];
-        if constexpr (OM == kOpsMix) {  // ops 1..6 at kL64Main
-            const uint4 *ops = reinterpret_cast<const uint4 *>(&pk->ops[1][0][0]);
-            for (uint32_t q = threadIdx.x; q < 6u * 128u; q += BLOCK) l4[kL64Main / 16 + q] = ops[q];
-        }
-        return;
-    }
-#if MCK_CRC64_P6
     // f6: entry v of table i at i*16 KiB + v*256 B, 32 copies (two per 16-B write)
     for (uint32_t q = threadIdx.x; q < 4096u; q += BLOCK) {
         const uint64_t v = pk->f6[q >> 10][(q >> 4) & 63u];
         l4[kL64P6 / 16 + q] = make_uint4((uint32_t)v, (uint32_t)(v >> 32), (uint32_t)v, (uint32_t)(v >> 32));
     }
     for (uint32_t d = threadIdx.x; d < 256u; d += BLOCK) l[kL64P5 / 8 + d] = pk->f5[d >> 5][d & 31u];
-#else
-    // low-nibble tables (main[2p]), 32 copies (two per ds_write_b128);
-    // high-nibble tables (main[2p+1]) at 16-B entry stride
-    for (uint32_t q = threadIdx.x; q < 2048u; q += BLOCK) {
-        const uint32_t d = q << 1;
-        const uint64_t v = pk->main[2 * (d >> 9)][(d >> 5) & 15u];
-        l4[q] = make_uint4((uint32_t)v, (uint32_t)(v >> 32), (uint32_t)v, (uint32_t)(v >> 32));
-    }
-    for (uint32_t d = threadIdx.x; d < 128u; d += BLOCK) {
-        const uint32_t p = d >> 4, v = d & 15u;  // table p, entry v
-        l[kL64Hi / 8 + (p & 3u) * 32 + (p >> 2) + v * 2] = pk->main[2 * p + 1][v];
-    }
-#endif
     if constexpr (OM == kOpsLds) {
         const uint4 *ops = reinterpret_cast<const uint4 *>(&pk->ops[0][0][0]);
         const uint32_t nops = pk->nops * 128u;
@@ -2112,27 +1475,21 @@ __device__ void fill_lds64(uint8_t *lds, const crc64_gpu_pack_t *pk) {
 __device__ __forceinline__ uint64_t lo64(uint4 v) { return (uint64_t)v.y << 32 | v.x; }
 __device__ __forceinline__ uint64_t hi64(uint4 v) { return (uint64_t)v.w << 32 | v.z; }
 
-// Load ring of the aligned CRC-64 loop: MCK_RING64_NT for the non-temporal
-// (>= 512 MiB) batches, MCK_RING64 otherwise (A/B knobs, round 4).
-#ifndef MCK_RING64_NT
-#define MCK_RING64_NT MCK_RING64
-#endif
-// Whole rings (K a multiple of the ring, K >= 2 rings): no load or step is
-// conditional, so the waitcnt pass sees one load per step and waits
-// vmcnt(R - 1) throughout.  In the merged segment kernel the general loop
-// below -- conditional ring fill and tail -- kept only one or two loads in
-// flight (vmcnt(1) in its steady loop, vmcnt(0) after the fill): +2.5% on
-// seg for the even form (profiles/r04/ab_seg_even.log).  MCK_A64_EVEN=0: the
-// general loop for every K.
-#ifndef MCK_A64_EVEN
-#define MCK_A64_EVEN 1
-#endif
-template <int LOG2G, bool NT, int OM, int FL = kFold12>
+// Aligned CRC-64 loop: a 4-deep ring of dwordx4 loads per lane, two 64-bit
+// sub-streams per lane.  Whole rings (K a multiple of the ring, K >= 2
+// rings) take payload64_even: no load or step is conditional, so the waitcnt
+// pass sees one load per step and waits vmcnt(R - 1) throughout.  In the
+// merged segment kernel the general loop -- conditional ring fill and tail --
+// kept only one or two loads in flight (vmcnt(1) in its steady loop,
+// vmcnt(0) after the fill): +2.5% on seg for the even form
+// (profiles/r04/ab_seg_even.log).
+constexpr int kRing64 = 4;
+template <int LOG2G, bool NT, int OM>
 __device__ __forceinline__ uint64_t payload64_even(const uint8_t *lds, const crc64_gpu_pack_t *pk, const uint8_t *p,
                                                    uint32_t K, uint32_t gl, uint32_t lc, uint64_t init) {
     constexpr int G = 1 << LOG2G;
-    constexpr int R = NT ? MCK_RING64_NT : MCK_RING64;
-    LaneT<FL> ln = lane_regs<FL>(lc);
+    constexpr int R = kRing64;
+    Lane64 ln = lane64(lc);
     gbyte_t src = global_ptr(p, LOG2G == 6) + 16u * gl;
     uint4 ring[R];
 #pragma unroll
@@ -2158,21 +1515,19 @@ __device__ __forceinline__ uint64_t payload64_even(const uint8_t *lds, const crc
     return combine64<LOG2G, OM>(lds, pk, x0, x1, gl);
 }
 
-template <int LOG2G, bool NT, int OM, int FL = kFold12>
+template <int LOG2G, bool NT, int OM>
 __device__ __forceinline__ uint64_t payload64_aligned(const uint8_t *lds, const crc64_gpu_pack_t *pk, const uint8_t *p,
                                                       uint32_t K, uint32_t gl, uint32_t lc, uint64_t init) {
     constexpr int G = 1 << LOG2G;
-    constexpr int R = NT ? MCK_RING64_NT : MCK_RING64;
-    if (MCK_A64_EVEN && MCK_LA64 && K % R == 0 && K >= 2 * R)
-        return payload64_even<LOG2G, NT, OM, FL>(lds, pk, p, K, gl, lc, init);
-    LaneT<FL> ln = lane_regs<FL>(lc);
+    constexpr int R = kRing64;
+    if (K % R == 0 && K >= 2 * R) return payload64_even<LOG2G, NT, OM>(lds, pk, p, K, gl, lc, init);
+    Lane64 ln = lane64(lc);
     // global (address-space 1) loads: a flat load would also hold up every LDS wait
     const gbyte_t src = global_ptr(p, LOG2G == 6) + 16u * gl;
     auto ldk = [&](uint32_t k) { return ldg16<NT>(src + (uint64_t)k * (16u * G)); };
     uint4 ring[R];
 #pragma unroll
     for (int u = 0; u < R; u++) ring[u] = (uint32_t)u < K ? ldk(u) : make_uint4(0, 0, 0, 0);
-#if MCK_LA64
     // x holds state ^ (the data word of the step about to run)
     uint64_t x0 = (gl == 0 ? init : 0ull) ^ lo64(ring[0]), x1 = hi64(ring[0]);
     uint32_t k = 0;
@@ -2196,82 +1551,7 @@ __device__ __forceinline__ uint64_t payload64_aligned(const uint8_t *lds, const 
             }
         }
     }
-#else
-    uint64_t x0 = gl == 0 ? init : 0ull, x1 = 0;
-    for (uint32_t k = 0; k < K; k += R) {
-#pragma unroll
-        for (int u = 0; u < R; u++) {
-            const uint4 v = ring[u];
-            const uint32_t kn = k + u + R;
-            if (kn < K) ring[u] = ldk(kn);
-            if (k + u < K) {
-                x0 = f64x(lds, x0 ^ lo64(v), 0, ln);
-                x1 = f64x(lds, x1 ^ hi64(v), 0, ln);
-            }
-        }
-    }
-#endif
     return combine64<LOG2G, OM>(lds, pk, x0, x1, gl);
-}
-
-// MCK_CRC64_L8: 64 lanes of 8 bytes per step (one state per lane; the pack
-// is the 32-lane one, whose stride tables advance 512 B), butterflies
-// Z^-(8 * 2^k) = ops[k], k = 0..5 -- the two-state loop's in-lane combine
-// (ops[0]) and its first five levels.  K steps of 512 B.
-typedef const __attribute__((address_space(1))) uint64_t *g64_t;
-template <bool NT>
-__device__ __forceinline__ uint64_t ldg8(g64_t p) {
-    if constexpr (NT) return __builtin_nontemporal_load(p);
-    else return *p;
-}
-#ifndef MCK_RING64_L8
-#define MCK_RING64_L8 8
-#endif
-template <int OM>
-__device__ __forceinline__ uint64_t combine64_l8(const uint8_t *lds, const crc64_gpu_pack_t *pk, uint64_t x, uint32_t gl) {
-#pragma unroll
-    for (int k = 0; k < 6; k++) {
-        const uint64_t other = __shfl_xor(x, 1 << k, 64);
-        const bool bit = (gl >> k) & 1u;
-        const uint64_t lo = bit ? other : x, hi = bit ? x : other;
-        x = lo ^ opm64<OM>(lds, pk, k, hi);
-    }
-    return x;
-}
-template <bool NT, int OM>
-__device__ __forceinline__ uint64_t payload64_l8(const uint8_t *lds, const crc64_gpu_pack_t *pk, const uint8_t *p,
-                                                 uint32_t K, uint32_t gl, uint32_t lc, uint64_t init) {
-    constexpr int R = MCK_RING64_L8;
-    Lane64 ln = lane64(lc);
-    g64_t src = (g64_t)global_ptr(p, true) + gl;
-    uint64_t ring[R];
-    if (K % R == 0 && K >= 2 * R) {  // whole rings: no conditional load (cf. payload64_even)
-#pragma unroll
-        for (int u = 0; u < R; u++) ring[u] = ldg8<NT>(src + u * 64);
-        uint64_t x = (gl == 0 ? init : 0ull) ^ ring[0];
-        for (uint32_t k = R; k < K; k += R) {
-            src += R * 64;
-#pragma unroll
-            for (int u = 0; u < R; u++) {
-                ring[u] = ldg8<NT>(src + u * 64);
-                x = f64x(lds, x, ring[(u + 1) % R], ln);
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < R; u++) x = f64x(lds, x, u + 1 < R ? ring[u + 1] : 0ull, ln);
-        return combine64_l8<OM>(lds, pk, x, gl);
-    }
-#pragma unroll
-    for (int u = 0; u < R; u++) ring[u] = (uint32_t)u < K ? ldg8<NT>(src + u * 64) : 0ull;
-    uint64_t x = (gl == 0 ? init : 0ull) ^ ring[0];
-    for (uint32_t k = 0; k < K; k += R) {
-#pragma unroll
-        for (int u = 0; u < R; u++) {
-            if (k + u + R < K) ring[u] = ldg8<NT>(src + (uint64_t)(k + u + R) * 64);
-            if (k + u < K) x = f64x(lds, x, k + u + 1 < K ? ring[(u + 1) % R] : 0ull, ln);
-        }
-    }
-    return combine64_l8<OM>(lds, pk, x, gl);
 }
 
 template <int LOG2G, bool NT, int OM = kOpsLds>
@@ -2344,7 +1624,7 @@ __device__ __forceinline__ uint64_t tail64(const uint8_t *lds, const crc64_gpu_p
 }
 
 // CRC-64 counterpart of payload32_g64 (a non-zero RAW `reg` needs len >= 8).
-template <bool NT, bool RAW = false, int OM = kOpsLds, int FL = kFold12>
+template <bool NT, bool RAW = false, int OM = kOpsLds>
 __device__ __forceinline__ uint64_t payload64_g64(const uint8_t *lds, const crc64_gpu_pack_t *pk, const uint8_t *p,
                                                   uint64_t len, uint32_t gl, uint32_t lc, uint64_t reg = 0ull) {
     const uint64_t init = RAW ? reg : pk->init;
@@ -2363,7 +1643,7 @@ __device__ __forceinline__ uint64_t payload64_g64(const uint8_t *lds, const crc6
     constexpr uint32_t R = kRingOff64;
 
     uint64_t x0 = 0, x1 = 0;
-    LaneT<FL> ln = lane_regs<FL>(lc);
+    Lane64 ln = lane64(lc);
     auto fold = [&](uint32_t kk, uint4 v) {
         uint64_t w0 = lo64(v), w1 = hi64(v);
         if (kk < kc0 || kk >= kc1) {  // wave-uniform: an edge step
@@ -2432,7 +1712,7 @@ __global__ __launch_bounds__(kBlk64<MODE * 16 + LOG2G>, kWpe64<MODE * 16 + LOG2G
         sacc[threadIdx.x] = 0;
         scnt[threadIdx.x] = 0;
     }
-    fill_lds64<S::block, S::ops_mode, S::fold>(lds, pk);
+    fill_lds64<S::block, S::ops_mode>(lds, pk);
     __syncthreads();
     MCK_STAMP(blockIdx.x * kWPB + (threadIdx.x >> 6), 1);
 
@@ -2482,14 +1762,13 @@ __global__ __launch_bounds__(kBlk64<MODE * 16 + LOG2G>, kWpe64<MODE * 16 + LOG2G
         const bool faulted =
             for_each_unit<true, false, true, SplitPlan>(&wgq, a.queue, units, wave, nw, [&](uint64_t u, uint32_t r) {
                 uint64_t p;
-                uint32_t q, lg;
-                splan.unit(u, &p, &q, &lg);
-                const uint32_t pieces = 1u << lg;
-                const uint64_t bytes = a.len >> lg;  // this payload's piece size (kSplitBytes, or a quarter in the tail)
+                uint32_t q;
+                splan.unit(u, &p, &q);
+                const uint32_t pieces = 1u << splan.psl;
+                const uint64_t bytes = a.len >> splan.psl;  // kSplitBytes
                 const uint8_t *src = a.base + p * a.stride + (uint64_t)q * bytes;
                 uint64_t x;
-                if constexpr (S::l8) x = payload64_l8<NT, S::ops_mode>(lds, pk, src, (uint32_t)(bytes >> 9), gl, lc, q == 0 ? pk->init : 0ull);
-                else x = payload64_aligned<6, NT, S::ops_mode, S::fold>(lds, pk, src, (uint32_t)(bytes >> 10), gl, lc, q == 0 ? pk->init : 0ull);
+                x = payload64_aligned<6, NT, S::ops_mode>(lds, pk, src, (uint32_t)(bytes >> 10), gl, lc, q == 0 ? pk->init : 0ull);
                 if (gl == 0) {
                     const uint64_t t = shift64(sp, x, (uint64_t)(pieces - 1 - q) * bytes) ^ (q == 0 ? xorout : 0ull);
                     if (in_wg) {
@@ -2516,10 +1795,8 @@ __global__ __launch_bounds__(kBlk64<MODE * 16 + LOG2G>, kWpe64<MODE * 16 + LOG2G
         const bool act = p < a.count;
         const uint64_t pc = act ? p : a.count - 1;
         uint64_t x;
-        if constexpr (S::l8)
-            x = payload64_l8<NT, S::ops_mode>(lds, pk, a.base + pc * a.stride, (uint32_t)(a.len >> 9), gl, lc, pk->init);
-        else if constexpr (MODE == kFixedAligned)
-            x = payload64_aligned<LOG2G, NT, S::ops_mode, S::fold>(lds, pk, a.base + pc * a.stride, (uint32_t)(a.len >> (4 + LOG2G)), gl, lc, pk->init);
+        if constexpr (MODE == kFixedAligned)
+            x = payload64_aligned<LOG2G, NT, S::ops_mode>(lds, pk, a.base + pc * a.stride, (uint32_t)(a.len >> (4 + LOG2G)), gl, lc, pk->init);
         else
             x = payload64_generic<LOG2G, NT>(lds, pk, a.base + pc * a.stride, a.len, gl, lc);
         if (act && gl == 0) emit<uint64_t, VERIFY>(a, p, x ^ xorout);

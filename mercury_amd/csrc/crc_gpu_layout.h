@@ -58,14 +58,6 @@ typedef struct {
      * bits 0..2 of bytes i and i+4 together a 64-entry table.              */
     uint64_t f5[8][32];               /* f5[j][v] = F(v << (8j + 3))         */
     uint64_t f6[4][64];               /* f6[i][v] = F((v&7) << 8i | (v>>3) << (8i+32)) */
-    /* 11-lookup form (the one-workgroup-per-CU kernels, round 5): f5[0..5]
-     * (bits 3..7 of bytes 0..5), then 7-bit tables over bits 0..6 of byte 6
-     * and of byte 7, and over {bits 0..2 of bytes 0 and 4, bit 7 of byte 6}
-     * and {bits 0..2 of bytes 1 and 5, bit 7 of byte 7}, and one 6-bit table
-     * over bits 0..2 of bytes 2 and 3.                                       */
-    uint64_t f7[4][128];              /* f7[0][v] = F(v << 48), f7[1][v] = F(v << 56),
-                                         f7[2+i][v] = F((v&7) << 8i | (v>>3&7) << (8i+32) | (v>>6) << (8i+55)) */
-    uint64_t f6b[64];                 /* f6b[v] = F((v&7) << 16 | (v>>3) << 24) */
 } crc64_gpu_pack_t;
 
 /* ---- register shifts Z^n for 0 <= n < 2^48 (scatter-gather combine) ----- */

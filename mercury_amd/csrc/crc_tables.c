@@ -268,16 +268,6 @@ crc64_gpu_pack_build(const crc_rmodel_t *m, int log2g, crc64_gpu_pack_t *out)
         for (v = 0; v < 64; v++)
             out->f6[p][v] = crc_op_apply(64, op, ((uint64_t) (v & 7) << (8 * p)) |
                                                      ((uint64_t) (v >> 3) << (8 * p + 32)));
-    for (v = 0; v < 128; v++) {
-        out->f7[0][v] = crc_op_apply(64, op, (uint64_t) v << 48);
-        out->f7[1][v] = crc_op_apply(64, op, (uint64_t) v << 56);
-        for (p = 0; p < 2; p++)
-            out->f7[2 + p][v] = crc_op_apply(64, op, ((uint64_t) (v & 7) << (8 * p)) |
-                                                         ((uint64_t) ((v >> 3) & 7) << (8 * p + 32)) |
-                                                         ((uint64_t) (v >> 6) << (8 * p + 55)));
-    }
-    for (v = 0; v < 64; v++)
-        out->f6b[v] = crc_op_apply(64, op, ((uint64_t) (v & 7) << 16) | ((uint64_t) (v >> 3) << 24));
     if (fill_nibble_op64(m, -8, out->ops[o++]))
         return -1;
     for (k = 0; k < log2g; k++)

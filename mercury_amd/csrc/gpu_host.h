@@ -30,19 +30,21 @@ constexpr uint32_t kQueueSlots = kStreamSlots;
 // completion.
 struct SlotState {
     uint64_t seq = 0;            // launches enqueued on the slot: launch s counts in bank s & 1
-    // MCK_SLOT_DONE: the launch itself stores the slot's completed-launch count
-    // to DevCtx::slot_done[slot] (crc_gpu_device.h, "Completion"), so the slot
-    // is idle once that word reaches seq.  Otherwise: an event recorded by the
-    // completion of the slot's latest launch (hipExtLaunchKernel stop event).
+    // recorded by the completion of the slot's latest launch (hipExtLaunchKernel stop event)
     hipEvent_t done = nullptr;
     std::atomic<bool> pending{false};  // handed out, launch not yet enqueued (its event not yet recorded)
 };
 
+// Locking: a call takes no lock on its common path.  The context, table packs
+// and extension tables are created once under g_mu and published through
+// atomics (double-checked); the slot pool has a mutex of its own per device,
+// held for the few host-side steps of queue_slot / slot_unissue.
 struct DevCtx {
-    bool init = false;
+    std::atomic<bool> init{false};
     int cus = 0;
-    void *pack[MCK_NMODELS][CRC_GPU_MAX_LOG2G + 1] = {};
-    void *ext[MCK_NMODELS] = {};  // mchecksum_gpu_ext.hip's per-model tables
+    std::atomic<void *> pack[MCK_NMODELS][CRC_GPU_MAX_LOG2G + 1] = {};
+    std::atomic<void *> ext[MCK_NMODELS] = {};  // mchecksum_gpu_ext.hip's per-model tables
+    std::mutex pool_mu;                         // the slot pool below
     // Work-queue slots of the batch kernels (WgQueue, crc_gpu_device.h):
     // kQueueSlots zeroed counter sets of two banks each: launch s on a slot
     // uses bank s & 1 and zeroes the other for launch s + 1.  A slot serves one
@@ -55,11 +57,10 @@ struct DevCtx {
     // and take the plain static split (crc_gpu_device.h, "Exclusivity").
     unsigned long long *queue = nullptr;        // 2 * kQBankBytes-aligned view of queue_mem
     void *queue_mem = nullptr;
-    unsigned long long *slot_done = nullptr;    // host-mapped, one word per slot (MCK_SLOT_DONE)
     SlotState slot[kQueueSlots];
     uint32_t nslots = kQueueSlots;              // slots in the pool (MCHECKSUM_GPU_QUEUE_SLOTS lowers it for tests)
-    std::vector<uint32_t> idle;                 // slots known idle; the most recently reaped on top (guarded by g_mu)
-    std::deque<uint32_t> in_flight;             // slots handed out, oldest first (guarded by g_mu)
+    std::vector<uint32_t> idle;                 // slots known idle; the most recently reaped on top (pool_mu)
+    std::deque<uint32_t> in_flight;             // slots handed out, oldest first (pool_mu)
     // diagnostics (mchecksum_gpu_queue_stats)
     long long n_slot = 0, n_noslot = 0, n_reaped = 0, n_busy_skip = 0;
 };
@@ -88,12 +89,11 @@ struct Param {
 #if MCK_QFAULT_TEST
 // Test builds: the injected failure of the next launch (g_mck_qfault_mode,
 // crc_gpu_device.h; each translation unit has its own copy) from
-// MCHECKSUM_GPU_QFAULT_MODE ("stall" = 1, "scanstall" = 2, else the give-up
-// = 0), in stream order.
+// MCHECKSUM_GPU_QFAULT_MODE ("stall" = 1, "scanstall" = 2, "stall+scanstall"
+// = 3, else the give-up = 0), in stream order.
 static inline void qfault_mode_to_device(hipStream_t s) {
-    const char *env = getenv("MCHECKSUM_GPU_QFAULT_MODE");
-    static unsigned int modes[3] = {0u, 1u, 2u};  // static: the async copy's source must outlive the call
-    const int k = !env ? 0 : strcmp(env, "stall") == 0 ? 1 : strcmp(env, "scanstall") == 0 ? 2 : 0;
+    static unsigned int modes[4] = {0u, 1u, 2u, 3u};  // static: the async copy's source must outlive the call
+    const int k = mck_settings()->qfault_mode & 3;
     const unsigned int *m = &modes[k];
     (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_mck_qfault_mode), m, sizeof(*m), 0, hipMemcpyHostToDevice, s);
 }
@@ -109,7 +109,7 @@ hipError_t launch_kernel(void (*k)(P...), dim3 grid, dim3 block, hipStream_t s, 
     return hipLaunchKernel(reinterpret_cast<const void *>(k), grid, block, argv, 0, s);
 }
 
-extern std::mutex g_mu;
+extern std::mutex g_mu;  // creation of contexts and tables only
 
 // Record a formatted error for mchecksum_gpu_last_error(); returns rc.
 int set_err(int rc, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
@@ -122,13 +122,13 @@ int gpu_model(const char *method, int *width);
 crc_rmodel_t gpu_rmodel(int idx);
 bool gpu_msb(int idx);
 int swap_outputs(void *dev_out, uint64_t count, int width, void *stream);
-// Current device's context (caller holds g_mu).
+// Current device's context, created on first use (takes g_mu then only).
 int device_ctx(DevCtx **out);
-// Model + device context + table pack for lanes-per-payload 2^log2g (takes g_mu).
+// Model + device context + table pack for lanes-per-payload 2^log2g (g_mu on creation only).
 int prologue(const char *method, int log2g, int *width, DevCtx **c, const void **pack);
 // Per-device, per-model extension tables (mchecksum_gpu_ext.hip): the
 // Z^n shift pack of a 32/64-bit model, the byte table of a 16-bit one
-// (caller holds g_mu).
+// (g_mu on creation only).
 int get_ext(DevCtx *c, int idx, const void **out);
 // Work-queue slot bank for one launch of a throughput (non-light) batch
 // kernel on `stream`, exclusive to that launch until it completes; empty
@@ -141,9 +141,6 @@ void slot_unissue(DevCtx *c, SlotRef &r);
 // Queue-fault count of mchecksum_gpu_ext.hip's kernels (their own copy of
 // g_mck_queue_faults) on the current device; -1 on error.
 long long ext_queue_faults();
-// Set a translation unit's copy of the slot pool base and completion words
-// (g_mck_qbase, g_mck_slot_done) on the current device.
-hipError_t ext_set_slot_globals(unsigned long long *qbase, unsigned long long *done_dev);
 // This host thread's fail-closed report word (mchecksum_gpu_set_error_word), or nullptr.
 uint32_t *error_word();
 

@@ -351,8 +351,7 @@ update_msb(const mck_model_t *m, const uint64_t *t, uint64_t reg, const uint8_t 
 static void
 log_error(const char *fmt, const char *arg)
 {
-    const char *lvl = getenv("MCHECKSUM_LOG_LEVEL");
-    if (lvl && (strcmp(lvl, "none") == 0 || strcmp(lvl, "0") == 0))
+    if (mck_settings()->log_quiet)
         return;
     fprintf(stderr, "# mchecksum error: ");
     fprintf(stderr, fmt, arg ? arg : "(null)");

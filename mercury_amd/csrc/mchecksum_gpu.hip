@@ -122,17 +122,20 @@ int device_ctx(DevCtx **out) {
     if (e != hipSuccess) return hip_err(e, "hipGetDevice");
     if (dev < 0 || dev >= kMaxDev) return set_err(MCHECKSUM_GPU_ENODEV, "device id %d out of range", dev);
     DevCtx &c = g_dev[dev];
-    if (!c.init) {
+    if (c.init.load(std::memory_order_acquire)) {
+        *out = &c;
+        return 0;
+    }
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!c.init.load(std::memory_order_relaxed)) {
         int cus = 0;
         e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         if (e != hipSuccess) return hip_err(e, "hipDeviceGetAttribute");
         c.cus = cus > 0 ? cus : 1;
         // tests only: a smaller slot pool (MCHECKSUM_GPU_QUEUE_SLOTS=n), so a
         // test can hold every slot in flight
-        if (const char *env = getenv("MCHECKSUM_GPU_QUEUE_SLOTS")) {
-            const long v = atol(env);
-            if (v >= 1 && v < (long)kQueueSlots) c.nslots = (uint32_t)v;
-        }
+        const uint32_t qs = mck_settings()->gpu_queue_slots;
+        if (qs >= 1 && qs < kQueueSlots) c.nslots = qs;
         // slots aligned to two banks, so a bank's partner is its address ^ kQBankBytes
         const size_t slot_bytes = (size_t)kQSlotWords * sizeof(unsigned long long);
         const size_t qbytes = (size_t)kQueueSlots * slot_bytes + slot_bytes;
@@ -141,32 +144,13 @@ int device_ctx(DevCtx **out) {
         if (e == hipSuccess)
             c.queue = reinterpret_cast<unsigned long long *>((reinterpret_cast<uintptr_t>(c.queue_mem) + slot_bytes - 1) /
                                                              slot_bytes * slot_bytes);
-#if MCK_SLOT_DONE
-        // the slots' completion words: host-mapped, written by the launches
-        // (crc_gpu_device.h, "Completion"), read by slot_idle
-        unsigned long long *done_dev = nullptr;
-        if (e == hipSuccess)
-            e = hipHostMalloc(reinterpret_cast<void **>(&c.slot_done), kQueueSlots * sizeof(unsigned long long),
-                              hipHostMallocCoherent | hipHostMallocMapped);
-        if (e == hipSuccess) {
-            memset(c.slot_done, 0, kQueueSlots * sizeof(unsigned long long));
-            e = hipHostGetDevicePointer(reinterpret_cast<void **>(&done_dev), c.slot_done, 0);
-        }
-        if (e == hipSuccess)
-            e = hipMemcpyToSymbol(HIP_SYMBOL(g_mck_qbase), &c.queue, sizeof(c.queue), 0, hipMemcpyHostToDevice);
-        if (e == hipSuccess)
-            e = hipMemcpyToSymbol(HIP_SYMBOL(g_mck_slot_done), &done_dev, sizeof(done_dev), 0, hipMemcpyHostToDevice);
-        if (e == hipSuccess) e = ext_set_slot_globals(c.queue, done_dev);
-#endif
         if (e != hipSuccess) {
             if (c.queue_mem) (void)hipFree(c.queue_mem);
-            if (c.slot_done) (void)hipHostFree(c.slot_done);
             c.queue_mem = nullptr;
             c.queue = nullptr;
-            c.slot_done = nullptr;
             return hip_err(e, "work-queue allocation");
         }
-        c.init = true;
+        c.init.store(true, std::memory_order_release);
     }
     *out = &c;
     return 0;
@@ -174,8 +158,13 @@ int device_ctx(DevCtx **out) {
 
 // Returns the device table pack for (model, log2g), building it on first use.
 int get_pack(DevCtx *c, int idx, int log2g, const void **pack) {
-    if (c->pack[idx][log2g]) {
-        *pack = c->pack[idx][log2g];
+    if (void *p = c->pack[idx][log2g].load(std::memory_order_acquire)) {
+        *pack = p;
+        return 0;
+    }
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (void *p = c->pack[idx][log2g].load(std::memory_order_relaxed)) {
+        *pack = p;
         return 0;
     }
     const mck_model_t &m = mck_models[idx];
@@ -204,26 +193,21 @@ int get_pack(DevCtx *c, int idx, int log2g, const void **pack) {
         if (d) (void)hipFree(d);
         return hip_err(e, "table upload");
     }
-    c->pack[idx][log2g] = d;
+    c->pack[idx][log2g].store(d, std::memory_order_release);
     *pack = d;
     return 0;
 }
 
 // Whether slot i is idle: handed to no launch that has not yet been enqueued,
-// and its latest launch is done with it -- MCK_SLOT_DONE: the slot's
-// completed-launch count, which that launch's last workgroup stores to
-// host-mapped memory, has reached the launches enqueued on it (a plain host
-// read); otherwise its `done` event, recorded by that launch's completion
-// (launch_kernel's stop event), queried without blocking.  Neither is a
-// device round trip, so it may run under g_mu.  A never-recorded event
-// reads as complete.
+// and its latest launch is done with it -- its `done` event, recorded by that
+// launch's completion (launch_kernel's stop event), queried without blocking:
+// not a device round trip, so it may run under the pool lock.  A
+// never-recorded event reads as complete.  (Late round 5 had the launch's
+// last workgroup store a completion word to host-mapped memory instead:
+// correct, +-0 without a profiler, not kept.)
 bool slot_idle(const DevCtx *c, uint32_t i) {
     const SlotState &s = c->slot[i];
     if (s.pending.load(std::memory_order_acquire)) return false;
-#if MCK_SLOT_DONE
-    // the slot's completed launches, stored by its latest launch's last workgroup
-    return __atomic_load_n(&c->slot_done[i], __ATOMIC_ACQUIRE) == s.seq;
-#endif
     const hipError_t e = hipEventQuery(s.done);
     if (e == hipSuccess) return true;
     if (e != hipErrorNotReady) (void)hipGetLastError();
@@ -242,7 +226,7 @@ SlotRef queue_slot(DevCtx *c, void *stream) {
         (void)hipGetLastError();
         st = hipStreamCaptureStatusNone;
     }
-    std::lock_guard<std::mutex> lk(g_mu);
+    std::lock_guard<std::mutex> lk(c->pool_mu);
     // A captured launch replays with these arguments, possibly on two graph
     // execs at once: no slot can be exclusive to it, so it takes the static
     // split (crc_gpu_device.h, "Exclusivity").
@@ -279,7 +263,7 @@ SlotRef queue_slot(DevCtx *c, void *stream) {
     }
     const uint32_t i = c->idle.back();
     SlotState &s = c->slot[i];
-    if (!MCK_SLOT_DONE && !s.done && hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess) {
+    if (!s.done && hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess) {
         (void)hipGetLastError();
         s.done = nullptr;
         c->n_noslot++;
@@ -309,7 +293,7 @@ void slot_issued(SlotRef &r) {
 // the slot goes straight back to the pool.
 void slot_unissue(DevCtx *c, SlotRef &r) {
     if (r.idx < 0) return;
-    std::lock_guard<std::mutex> lk(g_mu);
+    std::lock_guard<std::mutex> lk(c->pool_mu);
     SlotState &s = c->slot[r.idx];
     s.seq--;
     for (auto it = c->in_flight.end(); it != c->in_flight.begin();) {
@@ -340,24 +324,26 @@ struct KLaunch {
 };
 
 // MCHECKSUM_GPU_LOG2G=g: 2^g lanes per payload for every fixed batch (A/B)
-bool lg_forced() {
-    const char *env = getenv("MCHECKSUM_GPU_LOG2G");
-    return env && env[0];
-}
+bool lg_forced() { return mck_settings()->gpu_log2g >= 0; }
 
 int choose_log2g(size_t len, int width) {
-    const char *env = getenv("MCHECKSUM_GPU_LOG2G");
-    if (env && env[0]) {
-        const int v = atoi(env);
-        if (v >= 0 && v <= CRC_GPU_MAX_LOG2G) return v;
-    }
-    // CRC-32 (round 4, one-process sweeps of 2..64 lanes over 1-16 KiB
-    // payloads, profiles/r04/ab_fixed_log2g*.log): 4 lanes from 1 KiB to under
-    // 8 KiB (C2's 4 KiB -1.9%, 2 KiB -1.4% against 8 and 16 lanes), then
-    // about 32 steps per payload (8 KiB: 16 lanes -1.2%, 16 KiB: 32 lanes
-    // -5.6%, against 32 and 64); 64 lanes from 32 KiB (the headline).
+    if (lg_forced()) return mck_settings()->gpu_log2g;
+    // CRC-32, 1 KiB to under 8 KiB: 16 steps per payload -- 4 lanes at 1 KiB,
+    // 8 at 2 KiB, 16 at 4 KiB.  Round 6 timed these shapes on cold lines
+    // (4 copies of each batch read in turn, so no launch re-reads what the
+    // last one left in the 256 MiB Infinity Cache; tools/ab_variants.py
+    // --rotate 4, profiles/r06/ab_lgcold.log): C2's 4 KiB at 16 lanes 50.5 us
+    // against 61.6 at 4 (+22%), 2 KiB at 8 lanes +3%; round 4 had chosen 4
+    // lanes throughout from back-to-back replays of one batch, which the
+    // cache served (-1.9% for 16 lanes there).  From 8 KiB about 32 steps
+    // per payload (8 KiB: 16 lanes, 16 KiB: 32 -- both still the best cold),
+    // 64 lanes from 32 KiB (the headline).
     if (width == 32 && len >= 1024) {
-        if (len < 8192) return 2;
+        if (len < 8192) {
+            int lg = 2;
+            while (lg < 4 && ((size_t)512 << lg) <= len) lg++;
+            return lg;
+        }
         int lg = 0;
         while (lg < CRC_GPU_MAX_LOG2G && ((size_t)512 << (lg + 1)) <= len) lg++;
         return lg;
@@ -416,26 +402,20 @@ KLaunch pick_fixed(int log2g, bool aligned, bool nt, bool light) {
 // (profiles/r01/latency.json).  MCHECKSUM_GPU_LIGHT=0/1 overrides.
 constexpr uint64_t kLightMaxBytes = 16ull << 20;  // crossover ~24 MiB (latency.json)
 bool use_light(uint64_t batch_bytes, bool known) {
-    const char *env = getenv("MCHECKSUM_GPU_LIGHT");
-    if (env && env[0]) return env[0] == '1';
+    if (mck_settings()->gpu_light >= 0) return mck_settings()->gpu_light == 1;
     return known && batch_bytes <= kLightMaxBytes;
 }
 
 // Lanes per payload for the light layout: as many as keep K >= kRing whole steps.
 int light_log2g(size_t len) {
-    const char *env = getenv("MCHECKSUM_GPU_LOG2G");
-    if (env && env[0]) {
-        const int v = atoi(env);
-        if (v >= 0 && v <= CRC_GPU_MAX_LOG2G) return v;
-    }
+    if (lg_forced()) return mck_settings()->gpu_log2g;
     int lg = CRC_GPU_MAX_LOG2G;
     while (lg > 0 && ((size_t)16 << lg) * kRing > len) lg--;
     return lg;
 }
 
 bool use_nt(uint64_t batch_bytes) {
-    const char *env = getenv("MCHECKSUM_GPU_NT");
-    if (env && env[0]) return env[0] == '1';
+    if (mck_settings()->gpu_nt >= 0) return mck_settings()->gpu_nt == 1;
     return batch_bytes >= (512ull << 20);
 }
 
@@ -462,7 +442,6 @@ unsigned grid_for(const DevCtx *c, uint64_t waves_needed, const KLaunch &kl) {
 int repack(DevCtx *c, const char *method, int log2g, const void **pack) {
     int width = 0;
     const int idx = gpu_model(method, &width);
-    std::lock_guard<std::mutex> lk(g_mu);
     return get_pack(c, idx, log2g, pack);
 }
 
@@ -470,7 +449,6 @@ int prologue(const char *method, int log2g, int *width, DevCtx **c, const void *
     int idx = gpu_model(method, width);
     if (idx == -1) return set_err(MCHECKSUM_GPU_EMETHOD, "unknown hash method \"%s\"", method ? method : "(null)");
     if (idx < 0) return set_err(MCHECKSUM_GPU_EMETHOD, "method \"%s\" has no GPU kernel (32/64-bit only)", method);
-    std::lock_guard<std::mutex> lk(g_mu);
     int rc = device_ctx(c);
     if (rc) return rc;
     return get_pack(*c, idx, log2g, pack);
@@ -542,24 +520,18 @@ int do_offsets(const char *method, const void *base, const uint64_t *offsets, si
 // (crc64_batch_kernel<..., SPLIT>) once the batch is big enough for the
 // non-temporal path; MCHECKSUM_GPU_SPLIT=0/1 overrides.
 bool use_split(int width, int lg, bool aligned, bool nt, size_t len, size_t stride) {
-    const char *env = getenv("MCHECKSUM_GPU_SPLIT");
-    if (env && env[0] && env[0] != '1') return false;
+    const int forced = mck_settings()->gpu_split;
+    if (forced == 0) return false;
     const bool shape = width == 64 && lg == CRC_GPU_MAX_LOG2G && aligned && len % kSplitBytes == 0 &&
                        len / kSplitBytes >= 2 && len / kSplitBytes <= 64 && ((len / kSplitBytes) & (len / kSplitBytes - 1)) == 0 &&
                        stride % 16 == 0;
-    if (env && env[0] == '1') return shape;
-#ifndef MCK_SPLIT64
-#define MCK_SPLIT64 1
-#endif
-    return MCK_SPLIT64 && shape && nt;
+    if (forced == 1) return shape;
+    return shape && nt;
 }
 
 // MCHECKSUM_GPU_SPLIT_LDS=0: split CRC-64 pieces always combine through the
 // zeroed output (tests, A/B).
-bool use_split_lds() {
-    const char *env = getenv("MCHECKSUM_GPU_SPLIT_LDS");
-    return !(env && env[0] == '0');
-}
+bool use_split_lds() { return mck_settings()->gpu_split_lds != 0; }
 
 int launch_fixed(DevCtx *c, int idx, const void *pack, int width, int lg, const void *dev_base, size_t stride,
                  size_t len, size_t count, void *dev_out, void *stream, bool light) {
@@ -567,14 +539,7 @@ int launch_fixed(DevCtx *c, int idx, const void *pack, int width, int lg, const 
     // The aligned path needs whole steps and K = len/step a multiple of the
     // load ring depth; everything else takes the generic path.
     const bool aligned = ((uintptr_t)dev_base % 16 == 0) && (stride % 16 == 0 || count == 1) &&
-                         len >= step * kRing && (len % (step * kRing) == 0) && (len >> (4 + lg)) < (1ull << 31) && !getenv("MCHECKSUM_GPU_FORCE_GENERIC");
-    // the one-state CRC-64 loop at 64 lanes (MCK_CRC64_L8) steps 512 B: the
-    // 32-lane pack's stride tables
-    if (Shape<64, kFixedAligned, false, 6>::l8 && width == 64 && lg == 6 && aligned && !light) {
-        std::lock_guard<std::mutex> lk(g_mu);
-        const int rc = get_pack(c, idx, 5, &pack);
-        if (rc) return rc;
-    }
+                         len >= step * kRing && (len % (step * kRing) == 0) && (len >> (4 + lg)) < (1ull << 31) && !mck_settings()->gpu_force_generic;
     BatchArgs a{};
     a.base = (const uint8_t *)dev_base;
     a.stride = stride;
@@ -586,14 +551,9 @@ int launch_fixed(DevCtx *c, int idx, const void *pack, int width, int lg, const 
     const bool nt = !light && use_nt((uint64_t)len * count);
     uint32_t sl = 0;
     while ((kSplitBytes << sl) < len && sl < 63) sl++;
-    // (the split plan's tail pieces are a quarter size: up to 4x the units)
-    if (use_split(width, lg, aligned, nt, len, count > 1 ? stride : 16) && ((uint64_t)count << (sl + 2)) <= kMaxUnits) {
+    if (use_split(width, lg, aligned, nt, len, count > 1 ? stride : 16) && ((uint64_t)count << sl) <= kMaxUnits) {
         const void *shift = nullptr;
-        {
-            std::lock_guard<std::mutex> lk(g_mu);
-            int rc = get_ext(c, idx, &shift);
-            if (rc) return rc;
-        }
+        if (int rc = get_ext(c, idx, &shift)) return rc;
         a.shift = shift;
         a.split_log2 = sl;
         using S6 = Shape<64, kFixedAligned, false, 6>;
@@ -681,7 +641,6 @@ int mchecksum_gpu_prepare(const char *hash_method) {
     // ... and the extension tables every entry point may need (Z^n shift pack:
     // split CRC-64 pieces, segments, XDR; CRC-16 byte table: core headers),
     // so that no call captured into a graph uploads anything
-    std::lock_guard<std::mutex> lk(g_mu);
     int rc = device_ctx(&c);
     if (rc) return rc;
     const void *ext = nullptr;
@@ -733,7 +692,7 @@ int mchecksum_gpu_checksum_fixed(const char *hash_method, const void *dev_base, 
     const int lg0 = lg;
     if (!lg_forced())
         while (lg < CRC_GPU_MAX_LOG2G && ((count + (64u >> lg) - 1) >> (6 - lg)) < (uint64_t)c->cus * 16) lg++;
-    // (the pack for another width only: repack takes g_mu)
+    // (the pack for another width only: repack)
     if (lg != lg0 && (rc = repack(c, hash_method, lg, &pack))) return rc;
     return launch_fixed(c, gpu_model(hash_method, &width), pack, width, lg, dev_base, stride, len, count, dev_out,
                         stream, false);
@@ -760,6 +719,8 @@ int mchecksum_gpu_verify_messages(const char *hash_method, const void *dev_buf, 
 
 const char *mchecksum_gpu_last_error(void) { return t_err; }
 
+void mchecksum_gpu_reload_settings(void) { mck_settings_reload(); }
+
 int mchecksum_gpu_set_error_word(uint32_t *dev_word) {
     t_err_word = dev_word;
     return MCHECKSUM_GPU_OK;
@@ -781,10 +742,10 @@ long long mchecksum_gpu_queue_faults(void) {
 int mchecksum_gpu_queue_stats(long long *stats, size_t n) {
     if (!stats) return set_err(MCHECKSUM_GPU_EINVAL, "NULL pointer argument");
     if (!mchecksum_gpu_available()) return set_err(MCHECKSUM_GPU_ENODEV, "no HIP device");
-    std::lock_guard<std::mutex> lk(g_mu);
     DevCtx *c = nullptr;
     int rc = device_ctx(&c);
     if (rc) return rc;
+    std::lock_guard<std::mutex> lk(c->pool_mu);
     const long long v[MCHECKSUM_GPU_QSTAT_COUNT] = {c->n_slot, c->n_noslot, c->n_reaped, c->n_busy_skip,
                                                     (long long)c->in_flight.size()};
     for (size_t i = 0; i < n && i < MCHECKSUM_GPU_QSTAT_COUNT; i++) stats[i] = v[i];

@@ -81,6 +81,10 @@ struct SegArgs {
     // static split) and the caller's fail-closed word
     unsigned long long *queue;
     uint32_t *err_word;
+    // the scan's fault report of this call (ScanArgs): claim == scan_key(epoch,
+    // *gen - 1) means the scan gave up, so the chunk pass hashes nothing
+    const uint64_t *fault_claim, *gen;
+    uint64_t epoch;
 };
 
 // Exclusive prefix sums of segment bytes (P) and chunk counts (C), each
@@ -100,13 +104,10 @@ struct SegArgs {
 // (start not 16-B aligned or length not a multiple of 1 KiB).  The same
 // launch presets out[j] = init ^ xorout.  Round 3 ran this as a block-reduce
 // launch and a block-offset launch (4.8 + 8.5 us at 32768 segments, beside a
-// kernel boundary), round 2 as three.
-// (MCK_SCAN_PER 1 / 2 -- 4x / 2x the scan blocks -- measured +-0.1% on the
-// bench's 32768-segment lists, profiles/r05/scan_per/)
-#ifndef MCK_SCAN_PER
-#define MCK_SCAN_PER 4  // segments per scan thread
-#endif
-constexpr uint32_t kScanThreads = 256, kScanPer = MCK_SCAN_PER, kScanBlk = kScanThreads * kScanPer;
+// kernel boundary), round 2 as three.  (1 or 2 segments per scan thread --
+// 4x / 2x the scan blocks -- measured +-0.1% on the bench's 32768-segment
+// lists, profiles/r05/scan_per/.)
+constexpr uint32_t kScanThreads = 256, kScanPer = 4, kScanBlk = kScanThreads * kScanPer;
 constexpr uint32_t kDescWords = 8;  // per scan block: flag, aggregate (p, c, r), inclusive (p, c, r), pad
 
 __device__ __forceinline__ uint64_t seg_chunks(uint64_t l) { return (l + kChunk - 1) / kChunk; }
@@ -167,6 +168,13 @@ __device__ __forceinline__ uint64_t wave_last_le(const uint64_t *a, uint64_t n, 
     return lo;
 }
 
+// (readfirstlane returns int: cast through uint32_t so nothing sign-extends)
+__device__ __forceinline__ uint32_t uniform(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t uniform(uint64_t v) {
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
+    return (uint64_t)hi << 32 | lo;
+}
 __device__ __forceinline__ uint64_t ld_relaxed(const uint64_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -189,7 +197,7 @@ __device__ __forceinline__ bool seg_lookback(uint64_t *desc, uint64_t b, uint64_
 #if MCK_QFAULT_TEST
     // injected stall (MCHECKSUM_GPU_QFAULT_MODE=scanstall): this block never
     // publishes, so every later block waits out its deadline
-    const bool mute = g_mck_qfault_mode == 2u && b == fault_block;
+    const bool mute = (g_mck_qfault_mode & 2u) && b == fault_block;
 #else
     constexpr bool mute = false;
 #endif
@@ -269,7 +277,7 @@ __device__ __forceinline__ bool seg_lookback(uint64_t *desc, uint64_t b, uint64_
 // starts at or before it), and every thread then reads its own segments'
 // entries.  Round 3 ran a binary search over all of first[] in global memory
 // per segment: ~14 dependent loads, 15 of the pass's 17 us at 32768 segments.
-// The scan's arguments (one launch, or block 0 of a fused chunk pass).
+// The scan's arguments.
 struct ScanArgs {
     const uint64_t *len, *addr;
     uint64_t nseg;
@@ -286,24 +294,31 @@ struct ScanArgs {
     uint32_t width;
     uint64_t preset;
     uint32_t *err_word;
-    uint64_t *fault_claim;  // workspace word: the call's epoch once a fault was reported
+    uint64_t *fault_claim;  // workspace word: the call's key once a fault was reported
+    uint64_t *gen;          // workspace word: calls scanned in this workspace (the key's second half)
     uint64_t fault_block;
 };
-// A call's scan-side give-ups (a look-back in any scan block, a fused chunk
-// pass's wait in any workgroup) add 1 to the error word between them, as the
-// header promises per launch: the first to swap the call's epoch into the
-// claim word reports, the rest see the epoch already there.
-__device__ __forceinline__ void report_scan_fault(const ScanArgs &sa) {
-    if (!sa.err_word) return;
-    const uint64_t was = __hip_atomic_exchange(sa.fault_claim, sa.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (was != sa.epoch) atomicAdd(sa.err_word, 1u);
+// A call's key: its epoch and the workspace's call count.  A graph replays
+// its captured epoch, so the epoch alone cannot tell two replays apart
+// (ADVICE r5); the count moves on every scan, captured or not.
+__device__ __forceinline__ uint64_t scan_key(uint64_t epoch, uint64_t gen) {
+    return epoch ^ (gen * 0x9E3779B97F4A7C15ull) ^ 0xD1B54A32D192ED03ull;
+}
+// A call's scan-side give-ups (a look-back in any scan block) add 1 to the
+// error word between them, as the header promises per call: the first to
+// swap the call's key into the claim word reports, the rest see it already
+// there -- and the chunk pass, seeing it, hashes nothing (fail closed, and
+// no second deadline in the same call).
+__device__ __forceinline__ void report_scan_fault(const ScanArgs &sa, uint64_t gen) {
+    const uint64_t key = scan_key(sa.epoch, gen);
+    const uint64_t was = __hip_atomic_exchange(sa.fault_claim, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (was != key && sa.err_word) atomicAdd(sa.err_word, 1u);
 }
 // LDS scratch of one scan block: the object rows of its segments (4 x u64 +
 // u32 each) and a few broadcast words
 constexpr uint32_t kScanScratch = kScanBlk * (4 * 8 + 4) + 64;
 
-// Scan block b of nb.  Threads below kScanThreads do the work; a wider block
-// (the fused chunk pass, 1024 threads) only joins the barriers with the rest.
+// Scan block b of nb (kScanThreads threads).
 __device__ __forceinline__ void scan_block(const ScanArgs &sa, uint64_t b, uint64_t nb, uint8_t *scratch) {
     const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
     const bool act = tid < kScanThreads;
@@ -351,13 +366,18 @@ __device__ __forceinline__ void scan_block(const ScanArgs &sa, uint64_t b, uint6
     __syncthreads();
     uint64_t *ex = bc + 2;
     if (w == 0) {
+        // the workspace's call count, read before this block publishes: the
+        // last block bumps it only after its look-back saw every block's
+        // descriptor, so all blocks of the call read the same count
+        const uint64_t gen = uniform(ld_relaxed(sa.gen));
         uint64_t ep, ec, er;
         const bool ok = seg_lookback(sa.desc, b, sa.epoch, tp, tc, *rag, lane, &ep, &ec, &er, sa.fault_block);
         if (lane == 0) {
             ex[0] = ep;
             ex[1] = ec;
             ex[2] = er;
-            if (!ok) report_scan_fault(sa);  // fail closed: the scan is not trustworthy
+            if (!ok) report_scan_fault(sa, gen);  // fail closed: the scan is not trustworthy
+            if (b + 1 == nb) st_relaxed(sa.gen, gen + 1);
         }
     }
     __syncthreads();
@@ -431,47 +451,6 @@ __global__ __launch_bounds__(kScanThreads) void seg_scan(ScanArgs sa) {
     scan_block(sa, blockIdx.x, gridDim.x, scratch);
 }
 
-// Fused scan (lists of one scan block, round 5): block 0 of the chunk pass
-// runs the scan in its table LDS before filling it, then publishes the call's
-// epoch in its descriptor's spare word (after an agent-scope release by every
-// thread); every workgroup waits for that word before it reads the scan's
-// results -- a wait on block 0 only, which is dispatched before any other, and
-// bounded by the 1 s deadline (a give-up reports on the error word).  One
-// launch per call instead of two for the small lists a bulk handle usually
-// carries.  Returns false when the wait gave up.
-__device__ __forceinline__ void fused_scan_publish(const ScanArgs &sa, uint8_t *scratch) {
-    scan_block(sa, 0, 1, scratch);
-    // every wave's stores are complete at the barrier (workgroup-scope release:
-    // s_waitcnt vmcnt(0)); one agent-scope release then publishes them all
-    __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_store(sa.desc + 7, sa.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ bool fused_scan_wait(const ScanArgs &sa) {
-    __shared__ uint32_t ok_s;
-    if (threadIdx.x == 0) {
-        Deadline dl;
-        uint32_t ok = 1;
-        while (__hip_atomic_load(sa.desc + 7, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != sa.epoch) {
-            __builtin_amdgcn_s_sleep(2);
-            if (dl.passed()) {
-                queue_fault(14, blockIdx.x, sa.epoch);
-                ok = 0;
-                break;
-            }
-        }
-        ok_s = ok;
-    }
-    __syncthreads();
-    return ok_s != 0;
-}
-
-// (readfirstlane returns int: cast through uint32_t so nothing sign-extends)
-__device__ __forceinline__ uint32_t uniform(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane(v); }
-__device__ __forceinline__ uint64_t uniform(uint64_t v) {
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
-    return (uint64_t)hi << 32 | lo;
-}
 
 // A wave's contiguous range of chunks [c, c1), walked in order.  The segment
 // and object indices only advance, so a chunk costs a few cached scalar loads
@@ -517,20 +496,16 @@ struct ChunkWalk {
     }
 };
 
-// Work-queue chunk passes.  Chunks are the queue's units, so a wave holds
-// chunks from anywhere in the list and needs each one's segment and object
-// without walking: the scan writes both maps (SegArgs::obj, ::map), so a
-// chunk costs three dependent scalar loads.  A list with more chunks than the
-// map holds (segments far above 1 MiB on average) searches C instead.
+// Work-queue chunk pass (CRC-64).  Chunks are the queue's units, so a wave
+// holds chunks from anywhere in the list and needs each one's segment and
+// object without walking: the scan writes both maps (SegArgs::obj, ::map), so
+// a chunk costs three dependent scalar loads.  A list with more chunks than
+// the map holds (segments far above 1 MiB on average) searches C instead.
 // The first build searched C and first[] for every chunk (a guess plus a
 // gallop): its search loops pushed the 64-VGPR CRC-64 pass into 54 SGPR / 10
 // VGPR spills and it measured 5% slower than the static ranges
-// (profiles/r02/ab_seg_queue.log).  MCK_SEG_QUEUE=0 builds the static
-// contiguous ranges (ChunkWalk) for the A/B.
-#ifndef MCK_SEG_QUEUE
-#define MCK_SEG_QUEUE 1
-#endif
-
+// (profiles/r02/ab_seg_queue.log).
+//
 // Chunk c (< nchunks): its bytes [addr, addr + n) and, when its segment
 // belongs to an object (*in), the object, the object bytes after it (*end -
 // *stop) and whether it starts the object (*head).  c is wave-uniform, so
@@ -547,10 +522,9 @@ struct ChunkWalk {
 // payload loop whole-ring code (payload64_even, crc_gpu_device.h), now taken
 // for every chunk of whole rings (profiles/r04/ab_seg_locate_bound.log,
 // ab_seg_cheats.log, ab_seg_full.log, ab_seg_head.log, ab_seg_even.log).
-__device__ __forceinline__ __attribute__((unused)) void seg_locate(const SegArgs &a, uint64_t c, uint64_t nchunks,
-                                                                   uint64_t *addr, uint64_t *n, bool *in,
-                                                                   uint64_t *obj, uint64_t *end, uint64_t *stop,
-                                                                   bool *head) {
+__device__ __forceinline__ void seg_locate(const SegArgs &a, uint64_t c, uint64_t nchunks, uint64_t *addr,
+                                           uint64_t *n, bool *in, uint64_t *obj, uint64_t *end, uint64_t *stop,
+                                           bool *head) {
     const uint64_t s = nchunks <= a.map_cap ? (uint64_t)a.map[c] : lower_bound_u64(a.C, a.nseg + 1, c + 1) - 1;
     // (a scan whose look-back gave up -- reported on the error word -- leaves
     // maps that may not fit: such a chunk is skipped, never read out of bounds)
@@ -575,73 +549,34 @@ __device__ __forceinline__ __attribute__((unused)) void seg_locate(const SegArgs
     }
 }
 
-// PART 0: every chunk (CRC-32C: 140 KiB of LDS, one workgroup per CU either
-// way).  CRC-64, MCK_SEG_MERGED=1 (round 4): PART 3 takes every chunk from the
-// work queue in one 1024-thread workgroup per CU (128 VGPRs: the ragged loop
-// fits beside the aligned one; all operators in LDS).  MCK_SEG_MERGED=0 (round
-// 3) split the chunks by shape: PART 1 took the aligned ones with two
-// workgroups per CU (8 waves/SIMD, <= 64 VGPRs: only the aligned loop fits),
-// PART 2 the ragged ones in a launch of its own -- ~7 us per call even when
-// it found none (an early-exit launch of 256 x 1024 threads) -- while one
-// workgroup per CU ran the aligned CRC-64 loop as fast as two (C3, round 3:
-// +0.4% / +1.4%, profiles/r03/ab_crc64_one_wg_c3*.log).
-// (keyed W * 4 + PART: a comma inside __launch_bounds__ splits the macro)
-template <int KEY>
-constexpr int kSegWavesPerEU = KEY == 64 * 4 + 1 ? 8 : 1;
-#ifndef MCK_SEG_MERGED
-#define MCK_SEG_MERGED 1
-#endif
-
+// The chunk passes, one launch after the scan: one 1024-thread workgroup per
+// CU either way.  CRC-32C (140 KiB of LDS tables): each wave walks a static
+// contiguous range of chunks (ChunkWalk).  CRC-64 (round 4, "merged"): every
+// chunk from the work queue, the ragged loop beside the aligned one in 128
+// VGPRs and every operator in LDS.  (Round 3 split the CRC-64 chunks by
+// shape: the aligned ones at two workgroups per CU, the ragged ones in a
+// launch of their own -- ~7 us per call even when it found none.  Round 5
+// tried scanning inside the chunk pass for lists of one scan block: one
+// launch per call, but slower per call -- the other workgroups wait on block
+// 0's scan with an agent-scope acquire -- and not kept: HISTORY.md.)
 constexpr uint64_t kSegNtBytes = 512ull << 20;
 
-// FUSED: the list fits one scan block, and block 0 scans it in this launch
-// (fused_scan_*; `sa` is read only then).  Off by default: correct (the GPU
-// segment suites pass both ways) but slower per call than the scan launch --
-// 1 x 4 KiB CRC-32C 15.8 vs 13.6 us, CRC-64 25.5 vs 20.0 us, 1024 x 4 KiB
-// CRC-64 116 vs 72 us (tools/lat_seg.py, profiles/r05/lat_seg.json): the
-// other workgroups wait on block 0's scan with an agent-scope acquire, and
-// after it the compiler can no longer keep the chunk locates' workspace loads
-// scalar.  MCHECKSUM_GPU_SEG_FUSED=1 turns it on (tests).
-#ifndef MCK_SEG_FUSED
-#define MCK_SEG_FUSED 0
-#endif
-template <int W, int PART, bool FUSED = false>
-__global__ __launch_bounds__(1024, kSegWavesPerEU<W * 4 + PART>) void seg_kernel(SegArgs a, ScanArgs sa) {
-    // the table LDS; block 0 of a fused launch scans in it before the fill
-    constexpr bool OG = W == 64 && PART == 1 && MCK_CRC64_P6;
-    __shared__ __attribute__((aligned(16))) uint8_t lds_tab[W == 32 ? kL32Bytes : OG ? kL64Main : kL64Bytes];
-    if constexpr (FUSED) {
-        // block 0 scans first (its table fill follows); the others fill their
-        // tables while it does, and wait for its epoch after the fill
-        static_assert(sizeof(lds_tab) >= kScanScratch, "scan scratch in the table LDS");
-        if (blockIdx.x == 0) fused_scan_publish(sa, lds_tab);
-    } else {
-        (void)sa;
-        if (PART == 2 && *a.ragged == 0) return;  // every chunk takes the aligned pass
-    }
+template <int W>
+__global__ __launch_bounds__(1024, 1) void seg_kernel(SegArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds_tab[W == 32 ? kL32Bytes : kL64Bytes];
     constexpr int kWPB = 1024 / 64;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWPB + (threadIdx.x >> 6));
     const uint32_t nw = gridDim.x * kWPB;
-    uint64_t nchunks = FUSED ? 0 : uniform(a.C[a.nseg]);
-    // the CRC-64 aligned chunk pass takes chunks from the work queue (the host
-    // passes a slot; without one, for_each_unit strides statically)
-    constexpr bool kQueue = MCK_SEG_QUEUE && (PART == 1 || PART == 3);
+    const uint64_t nchunks = uniform(a.C[a.nseg]);
+    // the CRC-64 pass takes chunks from the work queue (the host passes a
+    // slot; without one, for_each_unit strides statically)
+    constexpr bool kQueue = W == 64;
     __shared__ WgQueue wgq;
-    if (!FUSED && kQueue && threadIdx.x == 0) wg_queue_init(&wgq, a.queue, nchunks);
-    // after the table fill (FUSED): the scan's results, then the queue
-    auto after_fill = [&]() -> bool {
-        if constexpr (FUSED) {
-            if (!fused_scan_wait(sa)) {
-                if (threadIdx.x == 0) report_scan_fault(sa);  // fail closed
-                return false;
-            }
-            nchunks = uniform(a.C[a.nseg]);
-            if (kQueue && threadIdx.x == 0) wg_queue_init(&wgq, a.queue, nchunks);
-            __syncthreads();
-        }
-        return true;
-    };
+    if (kQueue && threadIdx.x == 0) wg_queue_init(&wgq, a.queue, nchunks);
+    // the scan of this call gave up (reported on the error word): hash nothing
+    // -- after the queue's init, which readies the slot's other bank
+    if (uniform(ld_relaxed(a.fault_claim)) == scan_key(a.epoch, uniform(ld_relaxed(a.gen)) - 1)) return;
     // Calls body(addr, n, j, end, stop, head) for every chunk of this wave that
     // belongs to an object; true in the first wave of a launch whose queue
     // wait gave up (the caller's error word then gets +1: fail closed).
@@ -668,7 +603,6 @@ __global__ __launch_bounds__(1024, kSegWavesPerEU<W * 4 + PART>) void seg_kernel
         const crc32_shift_pack_t *sp = reinterpret_cast<const crc32_shift_pack_t *>(a.shift);
         fill_lds32<false, 1024>(lds_raw, pk);
         __syncthreads();
-        if (!after_fill()) return;
         const Tab32<false> lds{lds_raw};
         const uint32_t lc0 = (lane & 31u) << 2, lc1 = lc0 | 0x10000u;
         uint32_t *out = reinterpret_cast<uint32_t *>(a.out);
@@ -692,14 +626,11 @@ __global__ __launch_bounds__(1024, kSegWavesPerEU<W * 4 + PART>) void seg_kernel
         });
         if (faulted && lane == 0 && a.err_word) atomicAdd(a.err_word, 1u);
     } else {
-        // aligned chunks under the 12-lookup fold (PART 1): combine operators
-        // from global memory (once per 256 KiB chunk), so two workgroups fit a CU
         uint8_t *lds = lds_tab;
         const crc64_gpu_pack_t *pk = reinterpret_cast<const crc64_gpu_pack_t *>(a.pack);
         const crc64_shift_pack_t *sp = reinterpret_cast<const crc64_shift_pack_t *>(a.shift);
-        fill_lds64<1024, OG ? kOpsGlobal : kOpsLds>(lds, pk);
+        fill_lds64<1024, kOpsLds>(lds, pk);
         __syncthreads();
-        if (!after_fill()) return;
         const uint32_t lc = (lane & 31u) << 3;
         unsigned long long *out = reinterpret_cast<unsigned long long *>(a.out);
         // Non-temporal payload loads once the batch is far larger than the
@@ -707,19 +638,18 @@ __global__ __launch_bounds__(1024, kSegWavesPerEU<W * 4 + PART>) void seg_kernel
         // the device (the segment scan's total), so the choice is a uniform
         // branch per chunk: +3% on `seg` (duplicating the whole walk under one
         // branch measured the same and spills more).
-        [[maybe_unused]] const bool nt = uniform(a.P[a.nseg]) >= kSegNtBytes;
+        const bool nt = uniform(a.P[a.nseg]) >= kSegNtBytes;
         const uint64_t init = pk->init;
         const bool faulted = chunks([&](uint64_t p, uint64_t n, uint64_t j, uint64_t end, uint64_t stop, bool head) {
             const uint8_t *q = reinterpret_cast<const uint8_t *>(p);
             const bool aligned = p % 16 == 0 && n % 1024 == 0;
-            if (PART != 3 && aligned != (PART == 1)) return;
             // the object's first chunk starts from the register init (in its
             // first 8 bytes; Z^n(init) for a shorter, ragged chunk)
             const uint64_t reg = head && n >= 8 ? init : 0ull;
             uint64_t x;
-            if (PART == 1 || (PART == 3 && aligned))
-                x = nt ? payload64_aligned<6, true, OG>(lds, pk, q, (uint32_t)(n >> 10), lane, lc, reg)
-                       : payload64_aligned<6, false, OG>(lds, pk, q, (uint32_t)(n >> 10), lane, lc, reg);
+            if (aligned)
+                x = nt ? payload64_aligned<6, true, kOpsLds>(lds, pk, q, (uint32_t)(n >> 10), lane, lc, reg)
+                       : payload64_aligned<6, false, kOpsLds>(lds, pk, q, (uint32_t)(n >> 10), lane, lc, reg);
             else
                 x = payload64_g64<false, true>(lds, pk, q, n, lane, lc, reg);
             x = uniform(x);
@@ -984,10 +914,16 @@ __global__ __launch_bounds__(1024, 1) void xdr_fast_kernel(XdrArgs a) {
 namespace mck {
 
 // Per-device, per-model extension tables (shift pack for 32/64-bit models,
-// byte table for 16-bit ones), built and uploaded once under g_mu.
+// byte table for 16-bit ones), built and uploaded once (under g_mu), then
+// read without a lock.
 int get_ext(DevCtx *c, int idx, const void **out) {
-    if (c->ext[idx]) {
-        *out = c->ext[idx];
+    if (void *p = c->ext[idx].load(std::memory_order_acquire)) {
+        *out = p;
+        return 0;
+    }
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (void *p = c->ext[idx].load(std::memory_order_relaxed)) {
+        *out = p;
         return 0;
     }
     const mck_model_t &m = mck_models[idx];
@@ -1033,16 +969,9 @@ int get_ext(DevCtx *c, int idx, const void **out) {
         if (d) (void)hipFree(d);
         return hip_err(e, "table upload");
     }
-    c->ext[idx] = d;
+    c->ext[idx].store(d, std::memory_order_release);
     *out = d;
     return 0;
-}
-
-hipError_t ext_set_slot_globals(unsigned long long *qbase, unsigned long long *done_dev) {
-    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_mck_qbase), &qbase, sizeof(qbase), 0, hipMemcpyHostToDevice);
-    if (e == hipSuccess)
-        e = hipMemcpyToSymbol(HIP_SYMBOL(g_mck_slot_done), &done_dev, sizeof(done_dev), 0, hipMemcpyHostToDevice);
-    return e;
 }
 
 long long ext_queue_faults() {
@@ -1058,7 +987,8 @@ using namespace mck;
 
 extern "C" {
 
-// P, C (nseg + 1 each), the ragged flag, the scan's fault claim, the look-back descriptor of
+// P, C (nseg + 1 each), the ragged flag, the scan's fault claim, the workspace's
+// call count, a spare word, the look-back descriptor of
 // each scan block (kDescWords), each segment's object and its bounds in
 // first[] and its head segment (4 nseg), then the chunk -> segment map (u32 entries:
 // 4 per segment + 64 Ki, i.e. lists averaging up to ~1 MiB per segment, or
@@ -1071,12 +1001,11 @@ uint64_t seg_map_cap(uint64_t nseg) { return nseg < (1ull << 32) ? 4 * nseg + 65
 // b give up its look-back -- or, with MCHECKSUM_GPU_QFAULT_MODE=scanstall,
 // never publish its descriptor (tests/test_gpu_fail_closed.py); ~0 = none.
 uint64_t scan_fault_block() {
-    const char *env = MCK_QFAULT_TEST ? getenv("MCHECKSUM_GPU_QFAULT_SCAN") : nullptr;
-    return env && env[0] ? strtoull(env, nullptr, 10) : ~0ull;
+    return MCK_QFAULT_TEST ? mck_settings()->qfault_scan : ~0ull;
 }
 // scan blocks of a list (one at least: the scan launch writes the totals)
 uint64_t seg_blocks(uint64_t nseg) { return nseg ? (nseg + kScanBlk - 1) / kScanBlk : 1; }
-uint64_t seg_words(uint64_t nseg) { return 2 * (nseg + 1) + 2 + kDescWords * seg_blocks(nseg) + 4 * nseg; }
+uint64_t seg_words(uint64_t nseg) { return 2 * (nseg + 1) + 4 + kDescWords * seg_blocks(nseg) + 4 * nseg; }
 // The scan's look-back epochs: a process-wide counter from a random seed, so a
 // workspace's descriptors from any earlier call (this process or, through
 // reused memory, another) never match the current call's.
@@ -1111,10 +1040,7 @@ int mchecksum_gpu_checksum_segments(const char *hash_method, const uint64_t *dev
     const void *pack = nullptr, *shift = nullptr;
     int rc = prologue(hash_method, CRC_GPU_MAX_LOG2G, &width, &c, &pack);
     if (rc) return rc;
-    {
-        std::lock_guard<std::mutex> lk(g_mu);
-        rc = get_ext(c, mck_model_index(hash_method), &shift);
-    }
+    rc = get_ext(c, mck_model_index(hash_method), &shift);
     if (rc) return rc;
     if (nobj == 0) return MCHECKSUM_GPU_OK;
     hipStream_t s = (hipStream_t)stream;
@@ -1128,20 +1054,22 @@ int mchecksum_gpu_checksum_segments(const char *hash_method, const uint64_t *dev
     a.C = (const uint64_t *)dev_work + (nseg + 1);
     a.ragged = (const unsigned long long *)dev_work + 2 * (nseg + 1);
     const uint64_t nb = seg_blocks(nseg);
-    uint64_t *desc = (uint64_t *)dev_work + 2 * (nseg + 1) + 2;
+    uint64_t *desc = (uint64_t *)dev_work + 2 * (nseg + 1) + 4;
     a.obj = desc + kDescWords * nb;
     a.map = reinterpret_cast<const uint32_t *>((const uint64_t *)dev_work + seg_words(nseg));
     // only the CRC-64 queue pass reads the map; MCHECKSUM_GPU_SEG_MAP_CAP caps
     // the part of it used (tests: 0 forces the search over C)
-    a.map_cap = width == 64 && MCK_SEG_QUEUE ? seg_map_cap(nseg) : 0;
-    if (const char *env = getenv("MCHECKSUM_GPU_SEG_MAP_CAP")) {
-        const uint64_t v = strtoull(env, nullptr, 10);
+    a.map_cap = width == 64 ? seg_map_cap(nseg) : 0;
+    {
+        const uint64_t v = mck_settings()->gpu_seg_map_cap;
         a.map_cap = v < a.map_cap ? v : a.map_cap;
     }
     a.out = dev_out;
     a.pack = pack;
     a.shift = shift;
     a.err_word = error_word();
+    a.fault_claim = (const uint64_t *)dev_work + 2 * (nseg + 1) + 1;
+    a.gen = (const uint64_t *)dev_work + 2 * (nseg + 1) + 2;
     // every object starts as the CRC of the empty message, init ^ xorout in
     // the kernels' register form (MSB-first models: byte-reversed, swapped
     // back with the outputs below)
@@ -1152,62 +1080,37 @@ int mchecksum_gpu_checksum_segments(const char *hash_method, const uint64_t *dev
     sa.addr = dev_seg_addr;
     sa.nseg = nseg;
     sa.desc = desc;
-    sa.epoch = scan_epoch();
+    sa.epoch = a.epoch = scan_epoch();
     sa.P = (uint64_t *)a.P;
     sa.C = (uint64_t *)a.C;
     sa.ragged = (unsigned long long *)a.ragged;
     sa.first = dev_obj_first;
     sa.nobj = nobj;
-    sa.obj = width == 64 && MCK_SEG_QUEUE ? (uint64_t *)a.obj : nullptr;
+    sa.obj = width == 64 ? (uint64_t *)a.obj : nullptr;
     sa.map = (uint32_t *)a.map;
     sa.map_cap = a.map_cap;
     sa.out = dev_out;
     sa.width = (uint32_t)width;
     sa.preset = preset;
     sa.err_word = a.err_word;
-    sa.fault_claim = (uint64_t *)dev_work + 2 * (nseg + 1) + 1;
+    sa.fault_claim = (uint64_t *)a.fault_claim;
+    sa.gen = (uint64_t *)a.gen;
     sa.fault_block = scan_fault_block();
-    // A list of one scan block may be scanned by block 0 of the chunk pass
-    // itself (MCK_SEG_FUSED; MCHECKSUM_GPU_SEG_FUSED=0/1 overrides -- the tests
-    // run both).
-    const char *fenv = getenv("MCHECKSUM_GPU_SEG_FUSED");
-    const bool fused = nb == 1 && (width == 32 || MCK_SEG_MERGED) && (fenv && fenv[0] ? fenv[0] == '1' : MCK_SEG_FUSED);
-    hipError_t e = hipSuccess;
-    if (!fused) {
-        e = launch_kernel(seg_scan, dim3((unsigned)nb), dim3(kScanThreads), s, nullptr, sa);
-        if (e != hipSuccess) return hip_err(e, "segment scan launch");
-    }
+    hipError_t e = launch_kernel(seg_scan, dim3((unsigned)nb), dim3(kScanThreads), s, nullptr, sa);
+    if (e != hipSuccess) return hip_err(e, "segment scan launch");
     if (width == 32) {
-        e = fused ? launch_kernel(seg_kernel<32, 0, true>, dim3(c->cus), dim3(1024), s, nullptr, a, sa)
-                  : launch_kernel(seg_kernel<32, 0>, dim3(c->cus), dim3(1024), s, nullptr, a, sa);
-    } else if (MCK_SEG_MERGED) {
-        SlotRef sr = MCK_SEG_QUEUE ? queue_slot(c, stream) : SlotRef{};
-        a.queue = sr.q;
-        e = fused ? launch_kernel(seg_kernel<64, 3, true>, dim3(c->cus), dim3(1024), s, sr.done, a, sa)
-                  : launch_kernel(seg_kernel<64, 3>, dim3(c->cus), dim3(1024), s, sr.done, a, sa);
-        if (e != hipSuccess) {
-            slot_unissue(c, sr);
-            return hip_err(e, "segment kernel launch");
-        }
-        slot_issued(sr);
-    } else {
-        // the ragged pass first (it returns at once when the scan found no
-        // ragged chunk; XOR commutes, so the order of the passes is free): the
-        // call then ends on the long aligned pass, one kernel boundary fewer
-        // after it.  Only the aligned pass takes the work queue.
-        a.queue = nullptr;
-        e = launch_kernel(seg_kernel<64, 2>, dim3(c->cus), dim3(1024), s, nullptr, a, sa);
+        e = launch_kernel(seg_kernel<32>, dim3(c->cus), dim3(1024), s, nullptr, a);
         if (e != hipSuccess) return hip_err(e, "segment kernel launch");
-        SlotRef sr = MCK_SEG_QUEUE ? queue_slot(c, stream) : SlotRef{};
+    } else {
+        SlotRef sr = queue_slot(c, stream);
         a.queue = sr.q;
-        e = launch_kernel(seg_kernel<64, 1>, dim3(2 * c->cus), dim3(1024), s, sr.done, a, sa);
+        e = launch_kernel(seg_kernel<64>, dim3(c->cus), dim3(1024), s, sr.done, a);
         if (e != hipSuccess) {
             slot_unissue(c, sr);
             return hip_err(e, "segment kernel launch");
         }
         slot_issued(sr);
     }
-    if (e != hipSuccess) return hip_err(e, "segment kernel launch");
     // MSB-first model: the kernels' values are the CRCs byte-swapped (crc_gpu_layout.h)
     if (gpu_msb(mck_model_index(hash_method))) return swap_outputs(dev_out, nobj, width, stream);
     return MCHECKSUM_GPU_OK;
@@ -1229,13 +1132,8 @@ int mchecksum_gpu_verify_core_headers(const char *hash_method, int kind, const v
     if (!mchecksum_gpu_available()) return set_err(MCHECKSUM_GPU_ENODEV, "no HIP device");
     DevCtx *c = nullptr;
     const void *table = nullptr;
-    {
-        std::lock_guard<std::mutex> lk(g_mu);
-        int rc = device_ctx(&c);
-        if (rc) return rc;
-        rc = get_ext(c, idx, &table);
-        if (rc) return rc;
-    }
+    if (int rc = device_ctx(&c)) return rc;
+    if (int rc = get_ext(c, idx, &table)) return rc;
     if (count == 0) return MCHECKSUM_GPU_OK;
     HdrArgs a{};
     a.buf = (const uint8_t *)dev_buf;
@@ -1279,18 +1177,13 @@ int mchecksum_gpu_checksum_xdr(const char *hash_method, const mchecksum_xdr_fiel
     if (!mchecksum_gpu_available()) return set_err(MCHECKSUM_GPU_ENODEV, "no HIP device");
     DevCtx *c = nullptr;
     const void *shift = nullptr;
-    {
-        std::lock_guard<std::mutex> lk(g_mu);
-        int rc = device_ctx(&c);
-        if (rc) return rc;
-        rc = get_ext(c, idx, &shift);
-        if (rc) return rc;
-    }
+    if (int rc = device_ctx(&c)) return rc;
+    if (int rc = get_ext(c, idx, &shift)) return rc;
     if (count == 0) return MCHECKSUM_GPU_OK;
     // throughput layout for batches past a receive queue's worth of RPCs
     // (MCHECKSUM_GPU_XDR_FAST=0/1 overrides)
-    const char *fenv = getenv("MCHECKSUM_GPU_XDR_FAST");
-    const bool fast = fenv && fenv[0] ? fenv[0] == '1' : count > 1024;
+    const int fset = mck_settings()->gpu_xdr_fast;
+    const bool fast = fset >= 0 ? fset == 1 : count > 1024;
     if (fast) {
         int w2 = 0;
         const void *pack = nullptr;
@@ -1312,8 +1205,8 @@ int mchecksum_gpu_checksum_xdr(const char *hash_method, const mchecksum_xdr_fiel
     if (fast) {
         // non-temporal loads for batches far past the Infinity Cache, sized
         // by count as for offsets batches (MCHECKSUM_GPU_NT=0/1 overrides)
-        const char *nenv = getenv("MCHECKSUM_GPU_NT");
-        const bool nt = nenv && nenv[0] ? nenv[0] == '1' : count >= 8192;
+        const int nset = mck_settings()->gpu_nt;
+        const bool nt = nset >= 0 ? nset == 1 : count >= 8192;
         a.err_word = error_word();
         uint64_t blocks = (count + 15) / 16;
         if (blocks > (uint64_t)c->cus) blocks = (uint64_t)c->cus;

@@ -40,27 +40,113 @@ find(const char *name)
     return -1;
 }
 
+/* ------------------------------------------------------------ settings -- */
+
+static int
+env_int(const char *var, int lo, int hi)
+{
+    const char *e = getenv(var);
+    long v;
+
+    if (!e || !e[0])
+        return -1;
+    v = strtol(e, NULL, 10);
+    return v < lo || v > hi ? -1 : (int) v;
+}
+
+static int
+env_variant(const char *var, const char *family, const char *dflt)
+{
+    const char *e = getenv(var);
+
+    if (e && strncmp(e, family, 6) == 0 && find(e) >= 0)
+        return find(e);
+    return find(dflt);
+}
+
+static mck_settings_t *
+settings_from_env(void)
+{
+    mck_settings_t *s = calloc(1, sizeof(*s));
+    const char *e;
+
+    if (!s)
+        return NULL;
+    s->crc64_idx = env_variant("MCHECKSUM_CRC64_VARIANT", "crc64-", MCK_DEFAULT_CRC64);
+    s->crc16_idx = env_variant("MCHECKSUM_CRC16_VARIANT", "crc16-", MCK_DEFAULT_CRC16);
+    e = getenv("MCHECKSUM_LOG_LEVEL");
+    s->log_quiet = e && (strcmp(e, "none") == 0 || strcmp(e, "0") == 0);
+    s->gpu_log2g = env_int("MCHECKSUM_GPU_LOG2G", 0, CRC_GPU_MAX_LOG2G);
+    s->gpu_light = env_int("MCHECKSUM_GPU_LIGHT", 0, 1);
+    s->gpu_nt = env_int("MCHECKSUM_GPU_NT", 0, 1);
+    s->gpu_split = env_int("MCHECKSUM_GPU_SPLIT", 0, 1);
+    s->gpu_split_lds = env_int("MCHECKSUM_GPU_SPLIT_LDS", 0, 1) != 0;
+    s->gpu_force_generic = env_int("MCHECKSUM_GPU_FORCE_GENERIC", 0, 1) == 1;
+    s->gpu_xdr_fast = env_int("MCHECKSUM_GPU_XDR_FAST", 0, 1);
+    e = getenv("MCHECKSUM_GPU_SEG_MAP_CAP");
+    s->gpu_seg_map_cap = e && e[0] ? strtoull(e, NULL, 10) : UINT64_MAX;
+    e = getenv("MCHECKSUM_GPU_QUEUE_SLOTS");
+    s->gpu_queue_slots = e && e[0] && atol(e) > 0 ? (uint32_t) atol(e) : 0;
+    e = getenv("MCHECKSUM_GPU_QFAULT_MODE");
+    s->qfault_mode = !e                                  ? 0
+                     : strcmp(e, "stall") == 0           ? 1
+                     : strcmp(e, "scanstall") == 0       ? 2
+                     : strcmp(e, "stall+scanstall") == 0 ? 3
+                                                         : 0;
+    e = getenv("MCHECKSUM_GPU_QFAULT_SCAN");
+    s->qfault_scan = e && e[0] ? strtoull(e, NULL, 10) : UINT64_MAX;
+    return s;
+}
+
+/* The current snapshot.  A reload publishes a new one and never frees the
+ * old (a concurrent reader may still hold it): reloads are for tests and
+ * tuning tools, a few per process. */
+static const mck_settings_t *_Atomic g_settings;
+static pthread_once_t g_settings_once = PTHREAD_ONCE_INIT;
+static pthread_mutex_t g_settings_mu = PTHREAD_MUTEX_INITIALIZER;
+static const mck_settings_t g_settings_fallback = {.crc64_idx = 2, .crc16_idx = 11, .gpu_log2g = -1,
+                                                   .gpu_light = -1, .gpu_nt = -1, .gpu_split = -1,
+                                                   .gpu_split_lds = 1, .gpu_xdr_fast = -1,
+                                                   .gpu_seg_map_cap = UINT64_MAX, .qfault_scan = UINT64_MAX};
+
+static void
+settings_init(void)
+{
+    const mck_settings_t *s = settings_from_env();
+
+    __atomic_store_n(&g_settings, s ? s : &g_settings_fallback, __ATOMIC_RELEASE);
+}
+
+const mck_settings_t *
+mck_settings(void)
+{
+    pthread_once(&g_settings_once, settings_init);
+    return __atomic_load_n(&g_settings, __ATOMIC_ACQUIRE);
+}
+
+void
+mck_settings_reload(void)
+{
+    const mck_settings_t *s;
+
+    pthread_once(&g_settings_once, settings_init);
+    pthread_mutex_lock(&g_settings_mu);
+    s = settings_from_env();
+    if (s)
+        __atomic_store_n(&g_settings, s, __ATOMIC_RELEASE);
+    pthread_mutex_unlock(&g_settings_mu);
+}
+
 int
 mck_model_index(const char *hash_method)
 {
-    const char *name = hash_method;
-    int idx;
-
-    if (!name)
+    if (!hash_method)
         return -1;
-    if (strcmp(name, "crc64") == 0) {
-        const char *env = getenv("MCHECKSUM_CRC64_VARIANT");
-        name = MCK_DEFAULT_CRC64;
-        if (env && strncmp(env, "crc64-", 6) == 0 && find(env) >= 0)
-            name = env;
-    } else if (strcmp(name, "crc16") == 0) {
-        const char *env = getenv("MCHECKSUM_CRC16_VARIANT");
-        name = MCK_DEFAULT_CRC16;
-        if (env && strncmp(env, "crc16-", 6) == 0 && find(env) >= 0)
-            name = env;
-    }
-    idx = find(name);
-    return idx;
+    if (strcmp(hash_method, "crc64") == 0)
+        return mck_settings()->crc64_idx;
+    if (strcmp(hash_method, "crc16") == 0)
+        return mck_settings()->crc16_idx;
+    return find(hash_method);
 }
 
 uint64_t

@@ -15,6 +15,37 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device)")
 
 
+def reload_library_settings():
+    """libmchecksum reads its MCHECKSUM_* settings once per process; a test
+    that changes them re-reads them (mchecksum_gpu_reload_settings)."""
+    from mercury_amd import _lib
+    if _lib._lib is not None:
+        _lib.reload_settings()
+
+
+class _SettingsMonkeyPatch(pytest.MonkeyPatch):
+    """monkeypatch whose setenv / delenv of an MCHECKSUM_* variable, and whose
+    undo, make the library re-read its settings."""
+
+    def setenv(self, name, value, prepend=None):
+        super().setenv(name, value, prepend)
+        if name.startswith("MCHECKSUM_"):
+            reload_library_settings()
+
+    def delenv(self, name, raising=True):
+        super().delenv(name, raising)
+        if name.startswith("MCHECKSUM_"):
+            reload_library_settings()
+
+
+@pytest.fixture
+def monkeypatch():
+    mp = _SettingsMonkeyPatch()
+    yield mp
+    mp.undo()
+    reload_library_settings()
+
+
 @pytest.fixture(scope="session")
 def oracle_mod():
     from oracle import oracle as O

@@ -131,19 +131,8 @@ extern "C" uint64_t emu_crc64(const crc64_gpu_pack_t *pk, const uint8_t *buf, in
                 for (int p = 0; p < 8; p++) r6 ^= pk->f5[p][(x >> (8 * p + 3)) & 31];
                 for (int i = 0; i < 4; i++)
                     r6 ^= pk->f6[i][((x >> (8 * i)) & 7) | (((x >> (8 * i + 32)) & 7) << 3)];
-                // the 11-lookup form (f5[0..5], f7, f6b) with the kernels' own
-                // index formation (crc_gpu_device.h, f64x<kFold11>)
-                const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
-                uint64_t r7 = 0;
-                for (int p = 0; p < 6; p++) r7 ^= pk->f5[p][(x >> (8 * p + 3)) & 31];
-                r7 ^= pk->f7[0][(xh >> 16) & 0x7F] ^ pk->f7[1][(xh >> 24) & 0x7F];
-                const uint32_t t = (xl & 0x07070707u) | ((xh << 3) & ~0x07070707u);
-                const uint32_t t2 = (t & 0x3F3Fu) | ((xh >> 17) & ~0x3F3Fu);
-                r7 ^= pk->f7[2][t2 & 0x7F] ^ pk->f7[3][(t2 >> 8) & 0x7F];
-                const uint32_t t3 = (xl & 0x07070707u) | ((xl >> 5) & ~0x07070707u);
-                r7 ^= pk->f6b[(t3 >> 16) & 0x3F];
-                if (r6 != r || r7 != r) {
-                    std::fprintf(stderr, "emu_crc64: f5/f6 or 11-lookup fold differs from the nibble fold\n");
+                if (r6 != r) {
+                    std::fprintf(stderr, "emu_crc64: the f5/f6 fold differs from the nibble fold\n");
                     std::abort();
                 }
                 S[2 * l + j] = r6;

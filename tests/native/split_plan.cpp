@@ -1,7 +1,7 @@
 // Host check of the split CRC-64 queue plan (crc_gpu_device.h, SplitPlan):
 // for many batch shapes and grids, the chunks tile the units exactly once,
-// the units tile every payload's bytes exactly once (bulk pieces of
-// len / 2^psl, tail pieces of len / 2^tsl), and whenever whole() is true every
+// the units tile every payload's bytes exactly once (pieces of len / 2^psl),
+// and whenever whole() is true every
 // chunk holds whole payloads -- at most kSplitAcc, distinct mod kSplitAcc --
 // which the in-workgroup combine needs.  Built with hipcc for the host only.
 #include "crc_gpu_device.h"
@@ -24,13 +24,12 @@ int main() {
     const uint32_t grids[] = {1, 3, 8, 64, 255, 256, 512};
     const uint64_t counts[] = {1, 2, 5, 63, 100, 1000, 2048, 8192, 20000};
     const uint32_t psls[] = {1, 2, 3, 4, 6};
-    int shapes = 0, refined = 0, whole = 0;
+    int shapes = 0, whole = 0;
     for (uint32_t grid : grids)
         for (uint64_t count : counts)
             for (uint32_t psl : psls) {
                 const SplitPlan P(count, psl, grid);
                 shapes++;
-                refined += P.tsl != P.psl;
                 // chunks tile [0, n)
                 uint64_t next = 0;
                 for (uint64_t id = 0; id < P.nch; id++) {
@@ -42,18 +41,16 @@ int main() {
                 }
                 CHECK(next == P.n, "chunks end at %llu of %llu units (grid %u count %llu psl %u)",
                       (unsigned long long)next, (unsigned long long)P.n, grid, (unsigned long long)count, psl);
-                // units tile every payload in granules of len / 2^tsl
-                const uint32_t tsl = P.tsl, gran = 1u << tsl;
+                // units tile every payload in pieces of len / 2^psl
+                const uint32_t gran = 1u << P.psl;
                 std::vector<uint8_t> cover(count * gran, 0);
                 for (uint64_t u = 0; u < P.n; u++) {
                     uint64_t p;
-                    uint32_t q, lg;
-                    P.unit(u, &p, &q, &lg);
-                    CHECK(p < count && q < (1u << lg) && (lg == P.psl || lg == P.tsl), "unit %llu out of range",
-                          (unsigned long long)u);
+                    uint32_t q;
+                    P.unit(u, &p, &q);
+                    CHECK(p < count && q < gran, "unit %llu out of range", (unsigned long long)u);
                     if (p >= count) continue;
-                    const uint32_t per = 1u << (tsl - lg);  // granules per piece
-                    for (uint32_t g = 0; g < per; g++) cover[p * gran + q * per + g]++;
+                    cover[p * gran + q]++;
                 }
                 for (uint64_t i = 0; i < cover.size(); i++)
                     CHECK(cover[i] == 1, "granule %llu covered %d times (grid %u count %llu psl %u)",
@@ -66,8 +63,8 @@ int main() {
                     std::vector<uint32_t> seen;
                     for (uint64_t u = st; u < en; u++) {
                         uint64_t p;
-                        uint32_t q, lg;
-                        P.unit(u, &p, &q, &lg);
+                        uint32_t q;
+                        P.unit(u, &p, &q);
                         if (pays.empty() || pays.back() != p) {
                             pays.push_back(p);
                             seen.push_back(0);
@@ -77,30 +74,18 @@ int main() {
                     }
                     CHECK(pays.size() <= kSplitAcc, "chunk with %zu payloads", pays.size());
                     for (size_t k = 0; k < pays.size(); k++) {
-                        // the payload's piece count, from its first unit in the chunk
-                        uint32_t lg0 = 0;
-                        for (uint64_t u = st; u < en; u++) {
-                            uint64_t pp;
-                            uint32_t qq, ll;
-                            P.unit(u, &pp, &qq, &ll);
-                            if (pp == pays[k]) {
-                                lg0 = ll;
-                                break;
-                            }
-                        }
-                        CHECK(seen[k] == (1u << lg0), "payload %llu split over chunks (%u of %u pieces)",
-                              (unsigned long long)pays[k], seen[k], 1u << lg0);
+                        CHECK(seen[k] == gran, "payload %llu split over chunks (%u of %u pieces)",
+                              (unsigned long long)pays[k], seen[k], gran);
                         for (size_t j = 0; j < k; j++)
                             CHECK((pays[j] & (kSplitAcc - 1)) != (pays[k] & (kSplitAcc - 1)),
                                   "two payloads of a chunk share an accumulator");
                     }
                 }
             }
-    // C3's shape: the finer tail whenever it is on
+    // C3's shape: 4 pieces per payload, whole-payload chunks
     const SplitPlan c3(8192, 2, 256);
-    CHECK(c3.tsl == 2 + MCK_SPLIT_TAIL && c3.whole() && c3.n == 6144 * 4 + (2048ull << (2 + MCK_SPLIT_TAIL)),
-          "C3 plan: tsl %u n %llu", c3.tsl, (unsigned long long)c3.n);
-    printf("split plan: %d shapes (%d with finer tail pieces, %d whole-chunk), %d failures\n", shapes, refined, whole,
-           fails);
+    CHECK(c3.whole() && c3.n == 8192 * 4 && c3.cl == 5 && c3.sl == 2, "C3 plan: n %llu cl %u sl %u",
+          (unsigned long long)c3.n, c3.cl, c3.sl);
+    printf("split plan: %d shapes (%d whole-chunk), %d failures\n", shapes, whole, fails);
     return fails ? 1 : 0;
 }

@@ -90,11 +90,13 @@ def test_batch_arguments_rejected_before_any_device_work(product_lib):
     ]
     ws = L.mchecksum_gpu_segments_work_size
     ws.restype = ctypes.c_size_t
-    # P, C, flag, per scan block a look-back descriptor (8), segment -> (object, its first[] bounds, its head segment) (u64 words), then the
-    # chunk -> segment map (u32, 4 per segment + 64 Ki; none past 2^32 segments)
-    assert ws(4) == 8 * (2 * 5 + 2 + 8 + 4 * 4) + 4 * (4 * 4 + 65536) and ws((1 << 40) + 1) == (1 << 64) - 1
+    # P, C, ragged flag, fault claim, call count, spare, per scan block a
+    # look-back descriptor (8), segment -> (object, its first[] bounds, its head
+    # segment) (u64 words), then the chunk -> segment map (u32, 4 per segment +
+    # 64 Ki; none past 2^32 segments)
+    assert ws(4) == 8 * (2 * 5 + 4 + 8 + 4 * 4) + 4 * (4 * 4 + 65536) and ws((1 << 40) + 1) == (1 << 64) - 1
     n = 1 << 32
-    assert ws(n) == 8 * (2 * (n + 1) + 2 + 8 * (n // 1024) + 4 * n)
+    assert ws(n) == 8 * (2 * (n + 1) + 4 + 8 * (n // 1024) + 4 * n)
     first = (ctypes.c_uint64 * 2)(0, 1)
     cases += [
         (lambda: L.mchecksum_gpu_checksum_segments(b"crc64", offs, offs, 1, first, 1, buf, 8, buf, None), "workspace"),
@@ -116,8 +118,9 @@ def test_batch_arguments_rejected_before_any_device_work(product_lib):
 def test_lanes_per_payload_heuristic(product_lib):
     f = product_lib.mchecksum_gpu_lanes_per_payload
     assert f(b"crc32c", 65536) == 64
-    # CRC-32 (round-4 sweeps): 4 lanes from 1 KiB to under 8 KiB, then ~32 steps per payload
-    assert [f(b"crc32c", n) for n in (1024, 2048, 4096, 6144, 8192, 16384, 32768)] == [4, 4, 4, 4, 16, 32, 64]
+    # CRC-32 (round-6 sweeps on cold lines): 16 steps per payload from 1 KiB to
+    # under 8 KiB, then ~32 steps per payload
+    assert [f(b"crc32c", n) for n in (1024, 2048, 4096, 6144, 8192, 16384, 32768)] == [4, 8, 16, 16, 16, 32, 64]
     assert f(b"crc32c", 512) == 2
     # CRC-64: about 128 steps per payload, 4 lanes at least
     assert [f(b"crc64", n) for n in (1024, 4096, 16384, 65536, 262144)] == [4, 4, 8, 32, 64]

@@ -47,3 +47,27 @@ def test_find_package_consumer_links_and_runs(product_lib, tmp_path):
     r = subprocess.run([str(build / "consumer")], capture_output=True, text=True, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.strip() == "e3069283"
+
+
+@pytest.mark.skipif(shutil.which("cmake") is None, reason="cmake not installed")
+def test_batch_abi_consumer_builds_through_the_package(product_lib, tmp_path):
+    """The batch path's C binding (tests/native/hg_verify_consumer.c, the
+    INTEGRATION.md section 3 consumer) includes <mchecksum_gpu.h>, finds the
+    library through cmake/mchecksum-config.cmake, compiles with -Werror and
+    links libmchecksum + the HIP runtime.  On this GPU-less box it must see
+    every entry point refuse with MCHECKSUM_GPU_ENODEV (no host fallback);
+    tests/test_gpu_consumer.py runs the same program on the MI355X."""
+    build = tmp_path / "build"
+    src = os.path.join(ROOT, "tests", "native", "hg_consumer")
+    subprocess.run(["cmake", "-S", src, "-B", str(build), f"-Dmchecksum_DIR={os.path.join(ROOT, 'cmake')}"],
+                   check=True, capture_output=True)
+    subprocess.run(["cmake", "--build", str(build)], check=True, capture_output=True)
+    r = subprocess.run([str(build / "hg_verify_consumer")], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.startswith("NODEV"), r.stdout
+
+
+def test_batch_abi_consumer_is_built_in_tree():
+    """`make` leaves the consumer at build/hg_verify_consumer for the GPU box,
+    which runs the tree without building."""
+    assert os.access(os.path.join(ROOT, "build", "hg_verify_consumer"), os.X_OK), "run make"

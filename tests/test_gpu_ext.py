@@ -399,13 +399,11 @@ def test_segment_batch_calls_on_two_streams(gpu, buf, oracle_mod):
         assert gpu.as_unsigned(o).tolist() == want
 
 
-# Round 5: a list of one scan block (<= 1024 segments) can be scanned inside
-# the chunk pass (MCHECKSUM_GPU_SEG_FUSED=1, mchecksum_gpu_ext.hip: block 0
-# scans, every workgroup waits for its published epoch; off by default, it
-# measured slower than the separate scan launch).  Both paths vs the oracle.
+# Small lists around one scan block (<= 1024 segments per scan block): the
+# scan launch's look-back over one, exactly one and one-past-one blocks.
 @pytest.mark.parametrize("method", ["crc32c", "crc64", "crc64-ecma182"])
 @pytest.mark.parametrize("shape", ["one_segment", "few", "exactly_one_block", "one_past"])
-def test_segments_fused_scan_matches_scan_launch(gpu, buf, oracle_mod, method, shape, monkeypatch):
+def test_segments_around_one_scan_block(gpu, buf, oracle_mod, method, shape):
     host = _host(buf)
     import zlib
     rng = np.random.default_rng(zlib.crc32(f"{method}/{shape}".encode()))
@@ -420,24 +418,16 @@ def test_segments_fused_scan_matches_scan_launch(gpu, buf, oracle_mod, method, s
         first = sorted(set([0, n] + [int(x) for x in rng.integers(0, n, 40)]))
     want = _want(oracle_mod, method, host, segs, first)
     views = [buf[o:o + n] for o, n in segs]
-    monkeypatch.setenv("MCHECKSUM_GPU_SEG_FUSED", "1")
-    fused = gpu.as_unsigned(gpu.checksum_segments(method, views, first))
-    monkeypatch.setenv("MCHECKSUM_GPU_SEG_FUSED", "0")
-    launched = gpu.as_unsigned(gpu.checksum_segments(method, views, first))
-    assert fused.tolist() == want
-    assert launched.tolist() == want
+    assert gpu.as_unsigned(gpu.checksum_segments(method, views, first)).tolist() == want
 
 
-@pytest.mark.parametrize("fused", ["0", "1"])
 @pytest.mark.parametrize("method", ["crc32c", "crc64"])
-def test_segments_one_workspace_different_lists(gpu, buf, oracle_mod, method, fused, monkeypatch):
+def test_segments_one_workspace_different_lists(gpu, buf, oracle_mod, method):
     """One caller workspace reused by calls with different small lists, back to
-    back on one stream: every call must see its own scan (epoch-tagged; the
-    fused path's workgroups read the scan block 0 wrote in the same launch,
-    never the previous call's maps still cached)."""
+    back on one stream: every call must see its own scan (epoch-tagged
+    look-back descriptors, never the previous call's maps)."""
     import torch
     from mercury_amd import _lib
-    monkeypatch.setenv("MCHECKSUM_GPU_SEG_FUSED", fused)
     L = _lib.load_library()
     host = _host(buf)
     rng = np.random.default_rng(2026)

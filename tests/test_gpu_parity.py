@@ -31,27 +31,35 @@ def _dev_bytes(torch, host: np.ndarray, pad: int = 64):
     return t
 
 
-def _force_log2g(lg):
-    if lg is None:
-        os.environ.pop("MCHECKSUM_GPU_LOG2G", None)
+def _setenv(k, v):
+    """Set (or with v None, clear) a library setting; the library reads them
+    once, so it re-reads them here (conftest.reload_library_settings)."""
+    from conftest import reload_library_settings
+    if v is None:
+        os.environ.pop(k, None)
     else:
-        os.environ["MCHECKSUM_GPU_LOG2G"] = str(lg)
+        os.environ[k] = v
+    reload_library_settings()
+
+
+def _force_log2g(lg):
+    _setenv("MCHECKSUM_GPU_LOG2G", None if lg is None else str(lg))
 
 
 @pytest.fixture(autouse=True)
 def _clean_env():
     yield
     for k in ("MCHECKSUM_GPU_LOG2G", "MCHECKSUM_GPU_FORCE_GENERIC", "MCHECKSUM_GPU_LIGHT"):
-        os.environ.pop(k, None)
+        _setenv(k, None)
 
 
 @pytest.fixture(params=["full", "light"])
 def layout(request):
     """Both CRC-32C table layouts: the 32x-replicated throughput layout and the
     light small-batch layout (MCHECKSUM_GPU_LIGHT forces the choice)."""
-    os.environ["MCHECKSUM_GPU_LIGHT"] = "1" if request.param == "light" else "0"
+    _setenv("MCHECKSUM_GPU_LIGHT", "1" if request.param == "light" else "0")
     yield request.param
-    os.environ.pop("MCHECKSUM_GPU_LIGHT", None)
+    _setenv("MCHECKSUM_GPU_LIGHT", None)
 
 
 def test_selfcheck_small_known_answers(gpu, oracle_mod):
@@ -102,7 +110,7 @@ def test_fixed_unaligned_base_generic_path(gpu, oracle_mod, method, layout):
         got = gpu.as_unsigned(gpu.checksum_fixed(method, view, length, count=count))
         assert np.array_equal(got.astype(np.uint64), want), shift
     # the generic path forced on aligned data gives the same values
-    os.environ["MCHECKSUM_GPU_FORCE_GENERIC"] = "1"
+    _setenv("MCHECKSUM_GPU_FORCE_GENERIC", "1")
     want = oracle_mod.batch_fixed(method, host, length, length, count)
     got = gpu.as_unsigned(gpu.checksum_fixed(method, t, length, count=count))
     assert np.array_equal(got.astype(np.uint64), want)

@@ -5,16 +5,12 @@ unit is processed exactly once, no wait can block forever, and every launch
 leaves the bank the slot's next launch counts in at zero (two banks per slot,
 round 3: launch s counts in bank s & 1 and its first workgroup zeroes the
 other).  The host learns that a slot's launch is done with the slot from the
-HIP event its completion records (round 4) or, in MCK_SLOT_DONE=1 builds
-(crc_gpu_device.h "Completion without an event"), from the slot's completion
-word -- modelled here, as the stricter of the two: every wave counts itself
-out of its workgroup, the workgroup's last wave counts the workgroup out of its
-sub-queue group, the group's last out of the launch, and the launch's last
-workgroup bumps the slot's launch count and stores it to host-mapped memory
-(crc_gpu_device.h slot_exit).  The model checks that the word is stored once
-per launch, after the launch's last access to the slot, and that a launch
-handed the slot at that moment -- while the previous one's waves still run --
-is exact.
+HIP event its completion records (round 4), so the next launch on a slot
+starts after every wave of the previous one has ended.  Bounded waits are
+modelled in poll counts: a wait still unmet after `deadline` polls gives up
+and raises the launch's abort flag (round 6), and every other wait of the
+launch then gives up at its next clock read -- so a launch with a stall spends
+one deadline, not one per wait.
 
 Each wave is a generator that yields at every access to shared state (LDS or
 the global slot), so a seeded scheduler explores many orders of the same
@@ -48,19 +44,17 @@ class Bank:
     def zero(self):  # wg_queue_init, workgroup 0: the protocol lines only
         self.sub = [0] * QSUB          # sub-queue tickets
         self.fault = 0                 # first faulting wave of the launch
-        self.exit_group = [0] * QSUB   # workgroups counted out, per sub-queue group
-        self.exit_top = 0              # groups counted out
+        self.abort = 0                 # a wait of the launch gave up
 
     def clean(self):
-        return self.sub == [0] * QSUB and self.fault == 0 and self.exit_group == [0] * QSUB and self.exit_top == 0
+        return self.sub == [0] * QSUB and self.fault == 0 and self.abort == 0
 
 
 class Slot:
     def __init__(self):
         self.banks = [Bank(), Bank()]
         self.issued = 0       # launches handed this slot (host: SlotState::seq)
-        self.launches = 0     # device: the slot's completed-launch line (kQLaunchLine)
-        self.done = 0         # host-mapped completion word (DevCtx::slot_done)
+        self.active = False   # a launch on the slot has waves left (its completion event not yet recorded)
 
     def clean(self):
         """Ready for the next launch (the previous one has completed): the bank
@@ -70,7 +64,6 @@ class Slot:
 
 class Lds:
     def __init__(self):
-        self.exits = 0
         self.slot = 0
         self.drained = 0
         self.reads = [0] * RING
@@ -85,41 +78,38 @@ def run_model(n, grid, waves_per_wg, seed, slot=None, max_steps=2_000_000, drop=
     return res[0]["units"], res[0]["slot"]
 
 
-def run_launches(launches, seed, slot=None, max_steps=4_000_000):
-    """Several launches, their waves interleaved at random: at most one uses the
-    slot at a time (the host hands a slot to a launch only once the previous
-    launch's completion word says it is done with it); the others have none
-    (no_slot=True).  after_done=True: the launch is issued on the slot at the
-    moment the previous slot launch stores its completion word -- the host's
-    reap -- while that launch's waves may still run.  drop=(wg, seq): that
-    workgroup's wave taking slot 0 of chunk `seq` gives up (MCK_QFAULT_TEST)."""
+def run_launches(launches, seed, slot=None, max_steps=4_000_000, deadline=20_000):
+    """Several launches, their waves interleaved at random.  At most one uses the
+    slot at a time: a slot launch (no_slot absent) is issued only once every
+    wave of the previous one has ended (its completion event); launches with
+    no_slot=True take the static split beside it.  drop=(wg, seq): that
+    workgroup's wave taking slot 0 of chunk `seq` gives up (MCK_QFAULT_TEST
+    give-up).  stall=(wg, seq): that workgroup never publishes chunk seq + 1,
+    so the waves that take its slots wait out the deadline (MCK_QFAULT_TEST
+    "stall")."""
     rnd = random.Random(seed)
     slot = slot or Slot()
     clock = [0]
-    gens = []
     results = []
-    pending = []
+    pending = list(launches)
+    live = []  # [generators, result, uses_slot]
 
     def issue(spec):
-        r = dict(units=[], slot=slot, faulted_waves=0, first_faults=0, busy_wgs=0, last_access=-1, done_at=[])
+        r = dict(units=[], slot=slot, faulted_waves=0, first_faults=0, busy_wgs=0, gave_up_at=[], ended_at=0)
         results.append(r)
         bank = None
         if not spec.get("no_slot"):  # queue_slot: bank issued & 1, then count the launch
-            assert slot.done == slot.issued, "slot handed out while a launch still holds it"
+            assert not slot.active, "slot handed out while a launch still holds it"
             bank = (slot.banks[slot.issued & 1], slot.banks[(slot.issued & 1) ^ 1])
             slot.issued += 1
-        gens.extend(_launch(spec, bank, rnd, r, slot, clock))
+            slot.active = True
+        live.append([_launch(spec, bank, rnd, r, clock, deadline), r, bank is not None])
 
-    for spec in launches:
-        if spec.get("after_done"):
-            pending.append(spec)
-        else:
-            issue(spec)
-    while gens or pending:
-        if pending and slot.done == slot.issued:
+    while live or pending:
+        while pending and (pending[0].get("no_slot") or not slot.active):
             issue(pending.pop(0))
-            continue
-        assert gens, "a launch never stored its completion word"
+        launch = rnd.choice(live)
+        gens = launch[0]
         g = rnd.choice(gens)
         try:
             next(g)
@@ -127,13 +117,18 @@ def run_launches(launches, seed, slot=None, max_steps=4_000_000):
             gens.remove(g)
         clock[0] += 1
         assert clock[0] < max_steps, "no progress: a wait never ends"
+        if not gens:
+            live.remove(launch)
+            launch[1]["ended_at"] = clock[0]
+            if launch[2]:
+                slot.active = False  # the completion event
     for r in results:
         r["units"].sort()
     return results
 
 
-def _launch(spec, bank, rnd, res, slot, clock):
-    n, grid, waves_per_wg, drop = spec["n"], spec["grid"], spec["wpw"], spec.get("drop")
+def _launch(spec, bank, rnd, res, clock, deadline):
+    n, grid, waves_per_wg, drop, stall = spec["n"], spec["grid"], spec["wpw"], spec.get("drop"), spec.get("stall")
     cl = chunk_log2(n, grid)
     cu, lead = 1 << cl, max(1, (1 << cl) // 4) if (1 << cl) > 4 else 1
     # ChunkPlan: full chunks, then about one full chunk per workgroup of units
@@ -153,8 +148,19 @@ def _launch(spec, bank, rnd, res, slot, clock):
     lds = [Lds() for _ in range(grid)]
     cur, other = bank if bank else (None, None)
 
-    def touch():  # an access to the slot's lines
-        res["last_access"] = clock[0]
+    def wait(cond):
+        """A bounded wait (crc_gpu_device.h Deadline): True when cond() holds,
+        False once it gave up -- after `deadline` polls, or at the next poll
+        once the launch's abort flag is up (every 16th poll reads it)."""
+        polls = 0
+        while not cond():
+            polls += 1
+            if polls >= deadline or (polls % 16 == 1 and cur.abort):
+                cur.abort = 1  # raise_abort
+                res["gave_up_at"].append(clock[0])
+                return False
+            yield
+        return True
 
     def fetch(L, b):  # wg_fetch
         home = b % QSUB
@@ -165,7 +171,6 @@ def _launch(spec, bank, rnd, res, slot, clock):
             k = home if d == 0 else (home + 1 + (d - 1 + (b // QSUB) % (QSUB - 1)) % (QSUB - 1)) % QSUB
             t = cur.sub[k]
             cur.sub[k] += 1
-            touch()
             yield
             if k + t * QSUB < nch:
                 return k + t * QSUB
@@ -174,15 +179,16 @@ def _launch(spec, bank, rnd, res, slot, clock):
             d = max(L.drained, d + 1)
         return NOCH
 
-    def publish(L, seq, cid):  # wg_publish
+    def publish(L, seq, cid):  # wg_publish; False when its wait gave up
         r = seq % RING
+        ok = True
         if seq >= RING:
-            while L.reads[r] != cu:
-                yield
+            ok = yield from wait(lambda: L.reads[r] == cu)
         L.reads[r] = 0
         yield
         L.entry[r] = (seq, cid)
         yield
+        return ok
 
     def wave(b, w):  # for_each_unit<true>
         L = lds[b]
@@ -202,14 +208,18 @@ def _launch(spec, bank, rnd, res, slot, clock):
             L.slot += 1
             yield
             seq, r = t >> cl, (t >> cl) % RING
-            while L.entry[r][0] != seq:
-                yield
-            e = L.entry[r]
+            if (yield from wait(lambda: L.entry[r][0] == seq)):
+                e = L.entry[r]
+            else:
+                e = (seq, NOCH)
+                flt = True
             L.reads[r] += 1
             yield
             if (t & (cu - 1)) == cu - lead:
-                nid = NOCH if e[1] == NOCH else (yield from fetch(L, b))
-                yield from publish(L, seq + 1, nid)
+                stalled = stall is not None and (b, seq) == stall
+                nid = NOCH if e[1] == NOCH or stalled else (yield from fetch(L, b))
+                if not stalled and not (yield from publish(L, seq + 1, nid)):
+                    flt = True
             if drop is not None and (b, seq) == drop and (t & (cu - 1)) == 0:
                 flt = True  # injected give-up: this unit is never hashed
                 e = (seq, NOCH)
@@ -225,37 +235,8 @@ def _launch(spec, bank, rnd, res, slot, clock):
             res["faulted_waves"] += 1
             first = cur.fault == 0  # atomicCAS(fault, 0, 1)
             cur.fault = 1
-            touch()
             yield
             res["first_faults"] += first
-        # slot_exit: this wave, its workgroup, its group, the launch
-        L.exits += 1
-        last_wave = L.exits == waves_per_wg
-        yield
-        if not last_wave:
-            return
-        g = b % QSUB
-        in_group, groups = (grid - g + QSUB - 1) // QSUB, min(grid, QSUB)
-        old = cur.exit_group[g]
-        cur.exit_group[g] += 1
-        touch()
-        yield
-        if old != in_group - 1:
-            return
-        old = cur.exit_top
-        cur.exit_top += 1
-        touch()
-        yield
-        if old != groups - 1:
-            return
-        slot.launches += 1
-        n_done = slot.launches
-        touch()
-        yield
-        slot.done = n_done  # the host-mapped word
-        res["done_at"].append(clock[0])
-        for _ in range(rnd.randint(0, 20)):  # the launch's last waves may still run
-            yield
 
     def init(b):  # wg_queue_init (thread 0 of the workgroup, before the barrier)
         L = lds[b]
@@ -265,7 +246,6 @@ def _launch(spec, bank, rnd, res, slot, clock):
         else:
             if b == 0:
                 other.zero()  # the slot's next launch counts there
-                touch()
                 yield
             yield from publish(L, 0, (yield from fetch(L, b)))
         yield
@@ -339,30 +319,39 @@ def test_fault_flag_is_cleared_before_its_bank_is_reused():
     assert slot.banks[0].fault == 0 and slot.issued == 4
 
 
-@pytest.mark.parametrize("n,grid,wpw", [(1, 1, 1), (67, 5, 4), (1000, 9, 4), (5000, 8, 16), (20000, 12, 4),
-                                        (3000, 17, 2)])
-def test_completion_word_after_the_last_slot_access(n, grid, wpw):
-    """The launch's last workgroup stores the slot's launch count once, after
-    every access of the launch to the slot's lines (sub-queue tickets, the
-    fault flag, the exit counters, the next bank's zeroing)."""
-    slot = Slot()
-    for seed in range(3):
-        r = run_launches([dict(n=n, grid=grid, wpw=wpw)], seed * 104729 + n, slot)[0]
-        assert r["units"] == list(range(n))
-        assert len(r["done_at"]) == 1 and r["done_at"][0] > r["last_access"]
-        assert slot.done == slot.issued == seed + 1
-
-
-@pytest.mark.parametrize("seed", range(12))
-def test_next_launch_takes_the_slot_at_the_completion_word(seed):
-    """The host reaps the slot the moment the word is stored and hands it to the
-    next launch, whose waves then run beside the previous launch's last ones:
-    both hash every unit exactly once, and each stores its word once."""
-    specs = [dict(n=900, grid=6, wpw=4), dict(n=700, grid=5, wpw=4, after_done=True),
-             dict(n=1300, grid=9, wpw=2, after_done=True, drop=(1, 1)), dict(n=40, grid=3, wpw=4, after_done=True)]
+@pytest.mark.parametrize("seed", range(8))
+def test_next_slot_launch_after_completion(seed):
+    """Slot launches back to back (each issued at its predecessor's completion
+    event), one with a give-up, beside a slot-less launch: every launch hashes
+    each unit exactly once (the give-up's one unit aside) and the slot is clean
+    after each."""
+    specs = [dict(n=900, grid=6, wpw=4), dict(n=500, grid=3, wpw=4, no_slot=True), dict(n=700, grid=5, wpw=4),
+             dict(n=1300, grid=9, wpw=2, drop=(1, 1)), dict(n=40, grid=3, wpw=4)]
     res = run_launches(specs, seed * 7 + 3)
-    assert [r["units"] for r in res[:2]] == [list(range(900)), list(range(700))]
-    assert len(res[2]["units"]) == 1299 and res[2]["first_faults"] == 1
-    assert res[3]["units"] == list(range(40))
-    assert all(len(r["done_at"]) == 1 for r in res)
-    assert res[0]["slot"].done == res[0]["slot"].issued == 4
+    assert [r["units"] for r in res[:3]] == [list(range(900)), list(range(500)), list(range(700))]
+    assert len(res[3]["units"]) == 1299 and res[3]["first_faults"] == 1
+    assert res[4]["units"] == list(range(40))
+    assert res[0]["slot"].issued == 4 and res[0]["slot"].clean()
+
+
+@pytest.mark.parametrize("n,grid,wpw,stall", [(2000, 4, 4, (1, 0)), (5000, 8, 4, (3, 1)), (3000, 3, 16, (0, 2))])
+def test_stall_costs_one_deadline(n, grid, wpw, stall):
+    """A workgroup that never publishes a chunk (MCK_QFAULT_TEST "stall"): its
+    waves that take that chunk's slots wait out ONE deadline, the first give-up
+    raises the abort flag, and every other wait of the launch then gives up at
+    its next clock read -- the launch ends well within two deadlines, one wave
+    claims the fault, no unit is hashed twice, and the slot is clean after."""
+    deadline = 20_000
+    r = run_launches([dict(n=n, grid=grid, wpw=wpw, stall=stall)], n + grid, deadline=deadline)[0]
+    assert r["first_faults"] == 1 and r["faulted_waves"] >= 1
+    assert len(r["units"]) == len(set(r["units"])) and set(r["units"]) <= set(range(n))
+    assert r["gave_up_at"], "the stalled wait never gave up"
+    first = min(r["gave_up_at"])
+    # after the first give-up, every other waiting wave gives up within a few
+    # polls of its next clock read (16 polls), not after its own deadline
+    assert max(r["gave_up_at"]) - first < deadline // 2
+    assert r["ended_at"] - first < deadline // 2
+    assert r["slot"].banks[0].fault == 1 and r["slot"].banks[0].abort == 1  # zeroed by the slot's next launch
+    assert r["slot"].clean()
+    nxt = run_launches([dict(n=300, grid=2, wpw=4)], 5, r["slot"])[0]
+    assert nxt["units"] == list(range(300)) and nxt["first_faults"] == 0

@@ -49,6 +49,14 @@ SHAPES = {
 }
 
 
+def reload_settings(L):
+    """The library reads its MCHECKSUM_* settings once; re-read them (builds
+    from before round 6 read them on every call and have no such entry)."""
+    f = getattr(L, "mchecksum_gpu_reload_settings", None)
+    if f is not None:
+        f()
+
+
 def load(path):
     L = ctypes.CDLL(path)
     c = ctypes
@@ -71,6 +79,9 @@ def main():
     ap.add_argument("--env", nargs="*", default=[],
                     help="extra pseudo-variants of the default library: NAME=VAR=VALUE (env set around its calls)")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--rotate", type=int, default=1,
+                    help="fixed shapes: launch k reads copy k %% R of R equal batches at distinct addresses "
+                         "(cold lines: no launch re-reads what the last one left in the Infinity Cache)")
     ap.add_argument("--series", action="store_true",
                     help="one event pair around each round's back-to-back launches (bench.py's timing: the "
                          "boundaries between launches count) instead of one pair per launch")
@@ -115,8 +126,10 @@ def main():
             ref = G.checksum_offsets(method, data, offs, offsets_host=off_h)
         else:
             nbytes = count * length
-            data = torch.empty(count * length + 64, dtype=torch.uint8, device="cuda")
-            G.fill_splitmix(data, seed)
+            copies = [torch.empty(count * length + 64, dtype=torch.uint8, device="cuda") for _ in range(args.rotate)]
+            for d in copies:
+                G.fill_splitmix(d, seed)
+            data = copies[0]
             ref = G.checksum_fixed(method, data, length, count=count)
         torch.cuda.synchronize()
         stream = torch.cuda.current_stream()
@@ -129,6 +142,7 @@ def main():
             for n, L, o, e in zip(names, libs, outs, envs):
                 if e:
                     os.environ[e[0]] = e[1]
+                    reload_settings(L)
                 evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                        for _ in range(1 if args.series else args.iters)]
                 for k in range(args.iters):
@@ -140,7 +154,8 @@ def main():
                         rc = L.mchecksum_gpu_checksum_segments(method.encode(), mb, mb + 8 * ns, ns, mb + 16 * ns, seg.nobj,
                                                                seg.work.data_ptr(), seg.work.numel() * 8, o.data_ptr(), h)
                     elif offs is None:
-                        rc = L.mchecksum_gpu_checksum_fixed(method.encode(), data.data_ptr(), length, length, count,
+                        d = copies[k % len(copies)]
+                        rc = L.mchecksum_gpu_checksum_fixed(method.encode(), d.data_ptr(), length, length, count,
                                                             o.data_ptr(), h)
                     else:
                         rc = L.mchecksum_gpu_checksum_offsets(method.encode(), data.data_ptr(), offs.data_ptr(),
@@ -151,6 +166,7 @@ def main():
                 torch.cuda.synchronize()
                 if e:
                     del os.environ[e[0]]
+                    reload_settings(L)
                 if r > 0:  # round 0 = warm-up
                     times[n] += [a.elapsed_time(b) / (args.iters if args.series else 1) for a, b in evs]
         for n, o in zip(names, outs):
@@ -164,6 +180,7 @@ def main():
                   f"{res[n]['GBs_median']:.0f} GB/s (best {res[n]['GBs_best']:.0f})", flush=True)
         results[cfg] = res
         del data
+        copies = None
         torch.cuda.empty_cache()
     if args.out:
         json.dump(results, open(args.out, "w"), indent=1)
