@@ -125,8 +125,10 @@ struct BatchArgs {
 // Piece size of a split payload: 256 KiB = 256 steps of the G = 64 loop.
 // (A/B, round 4: 128 KiB pieces +2.9%, 512 KiB +6.8% on C3 time, profiles/r04/ab_split_piece.log)
 constexpr uint64_t kSplitBytes = 256u << 10;
-// Payloads per queue chunk whose pieces a workgroup can combine in LDS.
+// Payloads per queue chunk whose pieces a workgroup can combine in LDS, and
+// the accumulator sets (chunks with pieces in flight) it keeps.
 constexpr uint32_t kSplitAcc = 16;
+constexpr uint32_t kAccSets = 32;
 
 // ------------------------------------------------------------ work queue --
 // Dynamic distribution of payloads over waves.  With a static assignment the
@@ -526,137 +528,124 @@ __device__ __forceinline__ T wave_max(T v) {
 // q0 = min(n, nw) -- wg_queue_init gets n - q0 (first_static_units).
 __device__ __forceinline__ uint64_t first_static_units(uint64_t n, uint32_t nw) { return n < nw ? n : nw; }
 
-// DEFER (the split CRC-64 kernel's in-workgroup combine): body(u, r) gets
-// its chunk's ring entry r, and a taker counts itself a reader of the entry
-// only once body has returned -- the entry is not republished while any of
-// its units runs, so per-entry state in LDS outlives them all.
-template <bool DYN, bool FIRST = false, bool DEFER = false, class Plan = ChunkPlan, class F>
-__device__ __forceinline__ bool for_each_unit(WgQueue *L, unsigned long long *queue, uint64_t n, uint32_t wave,
-                                              uint32_t nw, F &&body, const Plan *given = nullptr) {
-    if constexpr (DYN) {
-        // One call site of body for both splits: a second inlined copy of the
-        // payload loop made the offsets kernels spill, and so does the copy
-        // loop unswitching makes -- hence busy is re-read from LDS every
-        // iteration (an atomic load the compiler cannot hoist).
-        const uint64_t q0 = FIRST ? first_static_units(n, nw) : 0;
-        uint64_t su = FIRST ? (uint64_t)wave + nw : wave;  // static cursor (busy slot)
-        const bool l0 = (threadIdx.x & 63u) == 0;
-        const Plan plan = [&] {
-            if constexpr (std::is_same_v<Plan, ChunkPlan>) return given ? *given : ChunkPlan(n - q0);
-            else return *given;
-        }();
-        const uint32_t cl = plan.cl, cu = 1u << cl, lead = cu > 4 ? cu / 4 : 1;
-        const uint64_t nch = plan.nch;
+// One wave's side of the queue protocol: take() takes the wave's next slot
+// (LDS counter), waits for its chunk in the ring, does the slot's fetch duty
+// and names the unit.  Without a slot (busy) it walks the static split.
+template <class Plan>
+struct UnitTaker {
+    WgQueue *L;
+    unsigned long long *queue;
+    uint64_t n, q0, su, nch, max_iters, iters = 0;
+    uint32_t nw, cl, cu, lead, flt = 0;  // flt (lane 0): a wait of this wave gave up
+    uint32_t seq = 0;                     // the workgroup's chunk sequence number of the last slot taken
+    bool l0;
+    Plan plan;
 #if MCK_TRACE
-        unsigned long long qs_n = 0, qs_sum = 0, qs_max = 0, qs_wait = 0, qs_busy = 0, qs_units = 0;
+    unsigned long long qs_n = 0, qs_sum = 0, qs_max = 0, qs_wait = 0, qs_busy = 0, qs_units = 0;
 #endif
-        const uint64_t max_iters = (uint64_t)cu * nch + 4ull * cu + 64;
-        uint64_t iters = 0;
-        uint32_t flt = 0;  // lane 0: a wait of this wave gave up
-        for (;;) {
-            uint64_t u;
-            uint32_t rr = 0, dfr = 0;  // DEFER: the unit's ring entry; lane 0: its read is still to count
-            (void)rr;
-            if (__builtin_amdgcn_readfirstlane(lds_ld(&L->busy))) {
-                if (su >= n) break;
-                u = su;
-                su += nw;
-            } else {
-                uint64_t e = 0;
-                uint32_t t = 0;
-                if (++iters > max_iters) {  // more slots than the launch has: protocol fault
-                    if (l0) {
-                        queue_fault(3, iters, 0);
-                        flt = 1;
-                    }
-                    break;
-                }
-                if (l0) {
-                    t = atomicAdd(&L->slot, 1u);
-                    const uint32_t seq = t >> cl, r = seq % kWgRing;
-                    Deadline dl(abort_word(queue));
+    __device__ __forceinline__ UnitTaker(WgQueue *L_, unsigned long long *q, uint64_t n_, uint32_t wave, uint32_t nw_,
+                                         bool first, const Plan &p)
+        : L(L_), queue(q), n(n_), q0(first ? first_static_units(n_, nw_) : 0),
+          su(first ? (uint64_t)wave + nw_ : wave), nch(p.nch), nw(nw_), cl(p.cl), cu(1u << p.cl),
+          lead(cu > 4 ? cu / 4 : 1), l0((threadIdx.x & 63u) == 0), plan(p) {
+        max_iters = (uint64_t)cu * nch + 4ull * cu + 64;
+    }
+    // The wave's next slot: false when the wave is done (the queue ran dry,
+    // or a wait gave up); else *u = its unit, or n for a tail chunk's slot
+    // past the chunk's size.  (busy is re-read from LDS every call -- an
+    // atomic load the compiler cannot hoist: one call site of the payload loop
+    // for both splits; a second inlined copy made the offsets kernels spill.)
+    __device__ __forceinline__ bool take(uint64_t *u) {
+        if (__builtin_amdgcn_readfirstlane(lds_ld(&L->busy))) {
+            if (su >= n) return false;
+            *u = su;
+            su += nw;
+            return true;
+        }
+        uint64_t e = 0;
+        uint32_t t = 0;
+        if (++iters > max_iters) {  // more slots than the launch has: protocol fault
+            if (l0) {
+                queue_fault(3, iters, 0);
+                flt = 1;
+            }
+            return false;
+        }
+        if (l0) {
+            t = atomicAdd(&L->slot, 1u);
+            const uint32_t seq = t >> cl, r = seq % kWgRing;
+            Deadline dl(abort_word(queue));
 #if MCK_TRACE
-                    const unsigned long long w0 = wall_clock64();
-                    unsigned long long f0 = 0;
+            const unsigned long long w0 = wall_clock64();
+            unsigned long long f0 = 0;
 #endif
-                    while (((e = lds_ld(&L->entry[r])) >> 32) != seq) {
-                        __builtin_amdgcn_s_sleep(1);
-                        MCK_WAIT_GUARD(dl, 2, seq, e)
-                    }
+            while (((e = lds_ld(&L->entry[r])) >> 32) != seq) {
+                __builtin_amdgcn_s_sleep(1);
+                MCK_WAIT_GUARD(dl, 2, seq, e)
+            }
 #if MCK_TRACE
-                    qs_wait += wall_clock64() - w0;
+            qs_wait += wall_clock64() - w0;
 #endif
-                    if ((e >> 32) != seq) {  // gave up (fault counted)
-                        raise_abort(queue);
-                        e = kNoChunk;
-                        flt = 1;
-                    }
-                    if constexpr (!DEFER) atomicAdd(&L->reads[r], 1u);
-                    // One taker per chunk (slot cu - lead) fetches the next
-                    // chunk -- after its own chunk is known, so fetches run in
-                    // chunk order and the first kNoChunk is final.
-                    if ((t & (cu - 1)) == cu - lead) {
+            if ((e >> 32) != seq) {  // gave up (fault counted)
+                raise_abort(queue);
+                e = kNoChunk;
+                flt = 1;
+            }
+            atomicAdd(&L->reads[r], 1u);
+            // One taker per chunk (slot cu - lead) fetches the next chunk --
+            // after its own chunk is known, so fetches run in chunk order and
+            // the first kNoChunk is final.
+            if ((t & (cu - 1)) == cu - lead) {
 #if MCK_TRACE
-                        f0 = wall_clock64();
+                f0 = wall_clock64();
 #endif
 #if MCK_QFAULT_TEST
-                        // injected stall: workgroup 3 neither fetches nor
-                        // publishes its third chunk (no chunk is lost: the
-                        // other workgroups take every unit), so each of its
-                        // waves waits out the deadline on that ring entry
-                        const bool stall = (g_mck_qfault_mode & 1u) && blockIdx.x == 3 && seq == 1;
+                // injected stall: workgroup 3 neither fetches nor publishes
+                // its third chunk (no chunk is lost: the other workgroups take
+                // every unit), so each of its waves waits out the deadline on
+                // that ring entry
+                const bool stall = (g_mck_qfault_mode & 1u) && blockIdx.x == 3 && seq == 1;
 #else
-                        constexpr bool stall = false;
+                constexpr bool stall = false;
 #endif
-                        const uint64_t nid =
-                            (e & 0xFFFFFFFFull) == kNoChunk || stall ? kNoChunk : wg_fetch(L, queue, nch);
+                const uint64_t nid = (e & 0xFFFFFFFFull) == kNoChunk || stall ? kNoChunk : wg_fetch(L, queue, nch);
 #if MCK_TRACE
-                        const unsigned long long df = wall_clock64() - f0;
-                        qs_n++;
-                        qs_sum += df;
-                        qs_max = df > qs_max ? df : qs_max;
+                const unsigned long long df = wall_clock64() - f0;
+                qs_n++;
+                qs_sum += df;
+                qs_max = df > qs_max ? df : qs_max;
 #endif
-                        if (!stall && !wg_publish(L, queue, seq + 1, nid, cl)) flt = 1;
-                    }
+                if (!stall && !wg_publish(L, queue, seq + 1, nid, cl)) flt = 1;
+            }
 #if MCK_QFAULT_TEST
-                    // injected give-up: workgroup 3 drops the first unit of its
-                    // second chunk (after its reads/publish duties, so the rest
-                    // of the launch runs on)
-                    if (g_mck_qfault_mode == 0u && blockIdx.x == 3 && seq == 1 && (t & (cu - 1)) == 0 && !flt) {
-                        queue_fault(9, seq, t);
-                        e = kNoChunk;
-                        flt = 1;
-                    }
-#endif
-                    if constexpr (DEFER) {  // a unit's read counts after its body; a skipped slot's now
-                        const uint64_t id0 = e & 0xFFFFFFFFull;
-                        dfr = id0 != kNoChunk && (t & (cu - 1)) < plan.size(id0);
-                        if (!dfr) atomicAdd(&L->reads[r], 1u);
-                    }
-                }
-                t = __builtin_amdgcn_readfirstlane(t);
-                const uint64_t id = uniform64(e) & 0xFFFFFFFFull;
-                if (id == kNoChunk) break;
-                // every chunk spans cu slots; a tail chunk's slots past its size are skipped
-                const uint32_t k = t & (cu - 1);
-                u = k < plan.size(id) ? q0 + plan.start(id) + k : n;
-                rr = (t >> cl) % kWgRing;
+            // injected give-up: workgroup 3 drops the first unit of its second
+            // chunk (after its reads/publish duties, so the rest of the launch
+            // runs on)
+            if (g_mck_qfault_mode == 0u && blockIdx.x == 3 && seq == 1 && (t & (cu - 1)) == 0 && !flt) {
+                queue_fault(9, seq, t);
+                e = kNoChunk;
+                flt = 1;
             }
-#if MCK_TRACE
-            const unsigned long long b0 = wall_clock64();
-#endif
-            if constexpr (DEFER) {
-                if (u < n) body(u, rr);
-                if (l0 && dfr) __hip_atomic_fetch_add(&L->reads[rr], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            } else {
-                if (u < n) body(u);
-            }
-#if MCK_TRACE
-            qs_busy += wall_clock64() - b0;
-            qs_units += u < n;
-            if (l0 && u < n && u < (1ull << 17)) g_mck_unit_end[u] = wall_clock64() | (unsigned long long)(blockIdx.x % kQSub) << 60;
 #endif
         }
+        t = __builtin_amdgcn_readfirstlane(t);
+        seq = t >> cl;
+        const uint64_t id = uniform64(e) & 0xFFFFFFFFull;
+        if (id == kNoChunk) return false;
+        // every chunk spans cu slots; a tail chunk's slots past its size are skipped
+        const uint32_t k = t & (cu - 1);
+        *u = k < plan.size(id) ? q0 + plan.start(id) + k : n;
+        return true;
+    }
+    // The wave's next unit, past any empty slots: false when it is done.
+    __device__ __forceinline__ bool take_unit(uint64_t *u) {
+        while (take(u))
+            if (*u < n) return true;
+        return false;
+    }
+    // After the wave's last take: true in the FIRST wave of the launch whose
+    // wait gave up (it claims the bank's fault flag and must run fail_closed).
+    __device__ __forceinline__ bool finish(uint32_t wave) {
 #if MCK_TRACE
         if (l0 && wave < 16384u) {
             g_mck_qwave[4 * wave] = qs_n;
@@ -666,18 +655,40 @@ __device__ __forceinline__ bool for_each_unit(WgQueue *L, unsigned long long *qu
             g_mck_qwave[4 * 16384 + 2 * wave] = qs_units;
             g_mck_qwave[4 * 16384 + 2 * wave + 1] = qs_busy;
         }
+#else
+        (void)wave;
 #endif
         if (__builtin_amdgcn_readfirstlane(lds_ld(&L->busy))) return false;  // no slot
-        // The first faulting wave of the launch claims the bank's fault flag.
         uint32_t first = 0;
         if (l0 && flt) first = atomicCAS(queue + kQFault * kQStride, 0ull, 1ull) == 0ull;
-        (void)nw;
         return __builtin_amdgcn_readfirstlane(first) != 0;
-    } else {
-        for (uint64_t u = FIRST ? (uint64_t)wave + nw : wave; u < n; u += nw) {
-            if constexpr (DEFER) body(u, 0u);
-            else body(u);
+    }
+};
+
+template <bool DYN, bool FIRST = false, class Plan = ChunkPlan, class F>
+__device__ __forceinline__ bool for_each_unit(WgQueue *L, unsigned long long *queue, uint64_t n, uint32_t wave,
+                                              uint32_t nw, F &&body, const Plan *given = nullptr) {
+    if constexpr (DYN) {
+        const Plan plan = [&] {
+            if constexpr (std::is_same_v<Plan, ChunkPlan>) return given ? *given : ChunkPlan(n - (FIRST ? first_static_units(n, nw) : 0));
+            else return *given;
+        }();
+        UnitTaker<Plan> tk(L, queue, n, wave, nw, FIRST, plan);
+        uint64_t u;
+        while (tk.take(&u)) {
+#if MCK_TRACE
+            const unsigned long long b0 = wall_clock64();
+#endif
+            if (u < n) body(u);
+#if MCK_TRACE
+            tk.qs_busy += wall_clock64() - b0;
+            tk.qs_units += u < n;
+            if (tk.l0 && u < n && u < (1ull << 17)) g_mck_unit_end[u] = wall_clock64() | (unsigned long long)(blockIdx.x % kQSub) << 60;
+#endif
         }
+        return tk.finish(wave);
+    } else {
+        for (uint64_t u = FIRST ? (uint64_t)wave + nw : wave; u < n; u += nw) body(u);
         return false;
     }
 }
@@ -1515,6 +1526,42 @@ __device__ __forceinline__ uint64_t payload64_even(const uint8_t *lds, const crc
     return combine64<LOG2G, OM>(lds, pk, x0, x1, gl);
 }
 
+// The split pieces' loop (G = 64, K a multiple of the ring and >= 2 rings):
+// ring64_load issues a piece's first kRing64 steps -- early, while the
+// previous piece still combines -- and fold64_ring runs the piece from them,
+// leaving the two sub-stream registers uncombined.
+template <bool NT>
+__device__ __forceinline__ void ring64_load(uint4 (&ring)[kRing64], const uint8_t *p, uint32_t gl) {
+    const gbyte_t src = global_ptr(p, true) + 16u * gl;
+#pragma unroll
+    for (int u = 0; u < kRing64; u++) ring[u] = ldg16<NT>(src + u * 1024u);
+}
+template <bool NT>
+__device__ __forceinline__ void fold64_ring(const uint8_t *lds, uint4 (&ring)[kRing64], const uint8_t *p, uint32_t K,
+                                            uint32_t gl, Lane64 &ln, uint64_t init, uint64_t *s0, uint64_t *s1) {
+    constexpr int R = kRing64;
+    gbyte_t src = global_ptr(p, true) + 16u * gl;
+    uint64_t x0 = (gl == 0 ? init : 0ull) ^ lo64(ring[0]), x1 = hi64(ring[0]);
+    for (uint32_t k = R; k < K; k += R) {
+        src += R * 1024u;
+#pragma unroll
+        for (int u = 0; u < R; u++) {
+            ring[u] = ldg16<NT>(src + u * 1024u);
+            const uint4 nx = ring[(u + 1) % R];
+            x0 = f64x(lds, x0, lo64(nx), ln);
+            x1 = f64x(lds, x1, hi64(nx), ln);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < R; u++) {
+        const uint4 nx = u + 1 < R ? ring[u + 1] : make_uint4(0, 0, 0, 0);
+        x0 = f64x(lds, x0, lo64(nx), ln);
+        x1 = f64x(lds, x1, hi64(nx), ln);
+    }
+    *s0 = x0;
+    *s1 = x1;
+}
+
 template <int LOG2G, bool NT, int OM>
 __device__ __forceinline__ uint64_t payload64_aligned(const uint8_t *lds, const crc64_gpu_pack_t *pk, const uint8_t *p,
                                                       uint32_t K, uint32_t gl, uint32_t lc, uint64_t init) {
@@ -1705,12 +1752,16 @@ __global__ __launch_bounds__(kBlk64<MODE * 16 + LOG2G>, kWpe64<MODE * 16 + LOG2G
         if constexpr (SPLIT) wg_queue_init_plan(&wgq, a.queue, splan);
         else wg_queue_init(&wgq, a.queue, units);
     }
-    // split pieces combined in the workgroup (SPLIT, split_lds)
-    __shared__ unsigned long long sacc[SPLIT ? kWgRing * kSplitAcc : 1];
-    __shared__ unsigned int scnt[SPLIT ? kWgRing * kSplitAcc : 1];
-    if (SPLIT && threadIdx.x < kWgRing * kSplitAcc) {
+    // split pieces combined in the workgroup (SPLIT, split_lds): per set
+    // (chunk sequence number % kAccSets) and payload (% kSplitAcc) the XOR of
+    // the pieces' terms, their count and the owning chunk (sequence + 1; 0 free)
+    __shared__ unsigned long long sacc[SPLIT ? kAccSets * kSplitAcc : 1];
+    __shared__ unsigned int scnt[SPLIT ? kAccSets * kSplitAcc : 1];
+    __shared__ unsigned int stag[SPLIT ? kAccSets * kSplitAcc : 1];
+    if (SPLIT && threadIdx.x < kAccSets * kSplitAcc) {
         sacc[threadIdx.x] = 0;
         scnt[threadIdx.x] = 0;
+        stag[threadIdx.x] = 0;
     }
     fill_lds64<S::block, S::ops_mode>(lds, pk);
     __syncthreads();
@@ -1759,33 +1810,103 @@ __global__ __launch_bounds__(kBlk64<MODE * 16 + LOG2G>, kWpe64<MODE * 16 + LOG2G
             }
             return;
         }
-        const bool faulted =
-            for_each_unit<true, false, true, SplitPlan>(&wgq, a.queue, units, wave, nw, [&](uint64_t u, uint32_t r) {
-                uint64_t p;
-                uint32_t q;
-                splan.unit(u, &p, &q);
-                const uint32_t pieces = 1u << splan.psl;
-                const uint64_t bytes = a.len >> splan.psl;  // kSplitBytes
-                const uint8_t *src = a.base + p * a.stride + (uint64_t)q * bytes;
-                uint64_t x;
-                x = payload64_aligned<6, NT, S::ops_mode>(lds, pk, src, (uint32_t)(bytes >> 10), gl, lc, q == 0 ? pk->init : 0ull);
-                if (gl == 0) {
-                    const uint64_t t = shift64(sp, x, (uint64_t)(pieces - 1 - q) * bytes) ^ (q == 0 ? xorout : 0ull);
-                    if (in_wg) {
-                        // (one wave's LDS atomics are performed in order: a piece's
-                        // XOR lands before its count)
-                        const uint32_t ai = r * kSplitAcc + (uint32_t)(p & (kSplitAcc - 1));
+        // Pipelined (round 6): a wave takes its NEXT piece as soon as the
+        // current one's step loop ends and issues that piece's first loads,
+        // so their HBM round trip overlaps the current piece's lane combine,
+        // Z^n shift and accumulation (before, each 256 KiB piece waited one
+        // HBM latency at its start, after its predecessor's combine).  A
+        // taken piece's ring read counts at once (no deferred reader), so the
+        // accumulators are keyed by the chunk's sequence number instead of
+        // its ring entry: set seq % kAccSets, owner tag seq + 1.  A piece
+        // whose entry an older chunk still holds waits for it (bounded; the
+        // older chunk's pieces are all taken and never wait on this one); a
+        // newer owner means the pieces in flight spanned kAccSets chunks,
+        // impossible with <= 32 pieces in flight -- a fault, never a value.
+        const uint32_t pieces = 1u << splan.psl;
+        const uint64_t bytes = a.len >> splan.psl;  // kSplitBytes
+        const uint32_t K = (uint32_t)(bytes >> 10);
+        auto src_of = [&](uint64_t u, uint64_t *p, uint32_t *q) {
+            splan.unit(u, p, q);
+            return a.base + *p * a.stride + (uint64_t)*q * bytes;
+        };
+        UnitTaker<SplitPlan> tk(&wgq, a.queue, units, wave, nw, false, splan);
+        Lane64 ln = lane64(lc);
+        uint4 ring[kRing64];
+        uint64_t u, p = 0;
+        uint32_t q = 0;
+        bool have = tk.take_unit(&u);
+        uint32_t seq = tk.seq;
+        const uint8_t *src = have ? src_of(u, &p, &q) : a.base;
+        if (have) ring64_load<NT>(ring, src, gl);
+        while (have) {
+            uint64_t x0, x1;
+            fold64_ring<NT>(lds, ring, src, K, gl, ln, q == 0 ? pk->init : 0ull, &x0, &x1);
+            uint64_t un = 0, pn = 0;
+            uint32_t qn = 0;
+            const bool next = tk.take_unit(&un);
+            const uint32_t seqn = tk.seq;
+            const uint8_t *srcn = next ? src_of(un, &pn, &qn) : src;
+            if (next) ring64_load<NT>(ring, srcn, gl);  // in flight during the combine below
+            const uint64_t x = combine64<6, kOpsLds>(lds, pk, x0, x1, gl);
+            if (gl == 0) {
+                const uint64_t t = shift64(sp, x, (uint64_t)(pieces - 1 - q) * bytes) ^ (q == 0 ? xorout : 0ull);
+                if (in_wg) {
+                    const uint32_t ai = (seq % kAccSets) * kSplitAcc + (uint32_t)(p & (kSplitAcc - 1));
+                    const uint32_t me = seq + 1;
+                    Deadline dl(abort_word(a.queue));
+                    bool own = false;
+                    for (;;) {
+                        const uint32_t tg = lds_ld(&stag[ai]);
+                        if (tg == me) {
+                            own = true;
+                            break;
+                        }
+                        if (tg == 0u) {
+                            unsigned int expect = 0u;
+                            if (__hip_atomic_compare_exchange_strong(&stag[ai], &expect, me, __ATOMIC_ACQ_REL,
+                                                                     __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+                                own = true;
+                                break;
+                            }
+                            continue;
+                        }
+                        if (tg > me) {  // a newer chunk on this entry: fail closed
+                            queue_fault(16, seq, tg);
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
+                        if (dl.passed()) {  // the older chunk never finished
+                            queue_fault(17, seq, tg);
+                            raise_abort(a.queue);
+                            break;
+                        }
+                    }
+                    if (own) {
+                        // (one wave's LDS atomics are performed in order: a
+                        // piece's XOR lands before its count, the last piece's
+                        // reset before the entry's release)
                         __hip_atomic_fetch_xor(&sacc[ai], (unsigned long long)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         const uint32_t seen = __hip_atomic_fetch_add(&scnt[ai], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
                         if (seen == pieces - 1) {
                             out[p] = __hip_atomic_exchange(&sacc[ai], 0ull, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
                             __hip_atomic_store(&scnt[ai], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            __hip_atomic_store(&stag[ai], 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                         }
                     } else {
-                        atomicXor(out + p, (unsigned long long)t);
+                        tk.flt = 1;
                     }
+                } else {
+                    atomicXor(out + p, (unsigned long long)t);
                 }
-            }, &splan);
+            }
+            have = next;
+            u = un;
+            p = pn;
+            q = qn;
+            seq = seqn;
+            src = srcn;
+        }
+        const bool faulted = tk.finish(wave);
         if (faulted) fail_closed<false>(a);
         MCK_STAMP(blockIdx.x * kWPB + (threadIdx.x >> 6), 2);
         return;

@@ -577,25 +577,15 @@ __global__ __launch_bounds__(1024, 1) void seg_kernel(SegArgs a) {
     // the scan of this call gave up (reported on the error word): hash nothing
     // -- after the queue's init, which readies the slot's other bank
     if (uniform(ld_relaxed(a.fault_claim)) == scan_key(a.epoch, uniform(ld_relaxed(a.gen)) - 1)) return;
-    // Calls body(addr, n, j, end, stop, head) for every chunk of this wave that
-    // belongs to an object; true in the first wave of a launch whose queue
-    // wait gave up (the caller's error word then gets +1: fail closed).
+    // CRC-32C: calls body(addr, n, j, end, stop, head) for every chunk of
+    // this wave's static range that belongs to an object.
     auto chunks = [&](auto &&body) -> bool {
-        if constexpr (kQueue) {
-            return for_each_unit<true>(&wgq, a.queue, nchunks, wave, nw, [&](uint64_t c) {
-                uint64_t p, n, j = 0, end = 0, stop = 0;
-                bool in, head = false;
-                seg_locate(a, c, nchunks, &p, &n, &in, &j, &end, &stop, &head);
-                if (in) body(p, n, j, end, stop, head);
-            });
-        } else {
-            ChunkWalk walk(a, wave, nw, nchunks);
-            uint64_t p, n, j = 0, end = 0, stop = 0;
-            bool in, head = false;
-            while (walk.next(&p, &n, &in, &j, &end, &stop, &head))
-                if (in) body(p, n, j, end, stop, head);
-            return false;
-        }
+        ChunkWalk walk(a, wave, nw, nchunks);
+        uint64_t p, n, j = 0, end = 0, stop = 0;
+        bool in, head = false;
+        while (walk.next(&p, &n, &in, &j, &end, &stop, &head))
+            if (in) body(p, n, j, end, stop, head);
+        return false;
     };
     if constexpr (W == 32) {
         uint8_t *lds_raw = lds_tab;
@@ -640,23 +630,63 @@ __global__ __launch_bounds__(1024, 1) void seg_kernel(SegArgs a) {
         // branch measured the same and spills more).
         const bool nt = uniform(a.P[a.nseg]) >= kSegNtBytes;
         const uint64_t init = pk->init;
-        const bool faulted = chunks([&](uint64_t p, uint64_t n, uint64_t j, uint64_t end, uint64_t stop, bool head) {
-            const uint8_t *q = reinterpret_cast<const uint8_t *>(p);
-            const bool aligned = p % 16 == 0 && n % 1024 == 0;
+        // Pipelined (round 6, as the split CRC-64 pieces): a chunk of whole
+        // rings from an aligned start (every chunk of a list of 16-B aligned
+        // KiB-multiple segments) runs from a ring its predecessor loaded --
+        // the wave takes the next chunk and issues its first loads as soon as
+        // the current step loop ends, before the current chunk's lane combine,
+        // Z^n shift and output XOR.  Other chunks run on their own.
+        struct Chunk {
+            uint64_t p = 0, n = 0, j = 0, end = 0, stop = 0;
+            bool in = false, head = false, even = false;
+        };
+        auto locate = [&](uint64_t c, Chunk *k) {
+            seg_locate(a, c, nchunks, &k->p, &k->n, &k->in, &k->j, &k->end, &k->stop, &k->head);
+            k->even = k->in && k->p % 16 == 0 && k->n % (1024u * kRing64) == 0 && k->n >= 2048u * kRing64;
+        };
+        auto issue = [&](uint4 (&ring)[kRing64], const Chunk &k) {
+            if (nt) ring64_load<true>(ring, reinterpret_cast<const uint8_t *>(k.p), lane);
+            else ring64_load<false>(ring, reinterpret_cast<const uint8_t *>(k.p), lane);
+        };
+        UnitTaker<ChunkPlan> tk(&wgq, a.queue, nchunks, wave, nw, false, ChunkPlan(nchunks));
+        Lane64 ln = lane64(lc);
+        uint4 ring[kRing64];
+        uint64_t c = 0;
+        Chunk cur;
+        bool have = tk.take_unit(&c);
+        if (have) locate(c, &cur);
+        if (have && cur.even) issue(ring, cur);
+        while (have) {
+            const uint8_t *q = reinterpret_cast<const uint8_t *>(cur.p);
             // the object's first chunk starts from the register init (in its
             // first 8 bytes; Z^n(init) for a shorter, ragged chunk)
-            const uint64_t reg = head && n >= 8 ? init : 0ull;
-            uint64_t x;
-            if (aligned)
-                x = nt ? payload64_aligned<6, true, kOpsLds>(lds, pk, q, (uint32_t)(n >> 10), lane, lc, reg)
-                       : payload64_aligned<6, false, kOpsLds>(lds, pk, q, (uint32_t)(n >> 10), lane, lc, reg);
-            else
-                x = payload64_g64<false, true>(lds, pk, q, n, lane, lc, reg);
-            x = uniform(x);
-            if (!aligned && head && n < 8) x ^= pk->zinit[n];
-            x = shift64(sp, x, end - stop);  // (the object bytes after the chunk)
-            if (lane == 0) atomicXor(out + j, (unsigned long long)(head ? x ^ init : x));  // ^ init: cancels the preset's
-        });
+            const uint64_t reg = cur.head && cur.n >= 8 ? init : 0ull;
+            uint64_t x = 0, x0 = 0, x1 = 0;
+            const bool aligned = cur.p % 16 == 0 && cur.n % 1024 == 0;
+            if (cur.even) {
+                if (nt) fold64_ring<true>(lds, ring, q, (uint32_t)(cur.n >> 10), lane, ln, reg, &x0, &x1);
+                else fold64_ring<false>(lds, ring, q, (uint32_t)(cur.n >> 10), lane, ln, reg, &x0, &x1);
+            } else if (cur.in && aligned) {
+                x = payload64_aligned<6, false, kOpsLds>(lds, pk, q, (uint32_t)(cur.n >> 10), lane, lc, reg);
+            } else if (cur.in) {
+                x = payload64_g64<false, true>(lds, pk, q, cur.n, lane, lc, reg);
+            }
+            uint64_t cn = 0;
+            Chunk nxt;
+            const bool next = tk.take_unit(&cn);
+            if (next) locate(cn, &nxt);
+            if (next && nxt.even) issue(ring, nxt);  // in flight during the combine below
+            if (cur.in) {
+                if (cur.even) x = combine64<6, kOpsLds>(lds, pk, x0, x1, lane);
+                x = uniform(x);
+                if (!aligned && cur.head && cur.n < 8) x ^= pk->zinit[cur.n];
+                x = shift64(sp, x, cur.end - cur.stop);  // (the object bytes after the chunk)
+                if (lane == 0) atomicXor(out + cur.j, (unsigned long long)(cur.head ? x ^ init : x));  // ^ init: cancels the preset's
+            }
+            cur = nxt;
+            have = next;
+        }
+        const bool faulted = tk.finish(wave);
         if (faulted && lane == 0 && a.err_word) atomicAdd(a.err_word, 1u);
     }
 }

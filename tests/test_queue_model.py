@@ -355,3 +355,165 @@ def test_stall_costs_one_deadline(n, grid, wpw, stall):
     assert r["slot"].clean()
     nxt = run_launches([dict(n=300, grid=2, wpw=4)], 5, r["slot"])[0]
     assert nxt["units"] == list(range(300)) and nxt["first_faults"] == 0
+
+
+# ---- split CRC-64 pieces, pipelined (round 6) -------------------------------
+# crc64_batch_kernel<..., SPLIT>: unit u = piece (u % 2^psl) of payload
+# u >> psl.  A wave takes its NEXT piece (slot, ring entry, read counted at
+# once) as soon as its current piece's step loop ends, then combines the
+# current one and accumulates it into the workgroup's LDS entry
+# (seq % NA, payload % 16), owned by the chunk (tag seq + 1) until its last
+# piece stores the CRC.  Checked here under random interleavings: every
+# payload's pieces are all accumulated and its CRC stored exactly once, no
+# wait blocks forever, and no entry is ever claimed by a newer chunk while an
+# older one holds it (the device turns that into a fault).
+NA, ACC = 32, 16
+
+
+def _split_model(count, psl, grid, wpw, seed, max_steps=6_000_000, deadline=200_000):
+    n = count << psl
+    pieces = 1 << psl
+    rnd = random.Random(seed)
+    cl = chunk_log2(n, grid)
+    cu, lead = 1 << cl, (1 << cl) // 4 if (1 << cl) > 4 else 1
+    sl = cl - 3 if cl >= 3 else cl
+    assert (1 << psl) <= (1 << sl) and (1 << cl) // (1 << psl) <= ACC, "not a whole-payload plan"
+    tail = grid << cl
+    nbig = (n - tail) >> cl if n > tail else 0
+    big_end = nbig << cl
+    nch = nbig + ((n - big_end + (1 << sl) - 1) >> sl)
+
+    def start(cid):
+        return cid << cl if cid < nbig else big_end + ((cid - nbig) << sl)
+
+    def size(cid):
+        return 1 << cl if cid < nbig else 1 << sl
+    bank = Bank()
+    lds = [Lds() for _ in range(grid)]
+    acc = [[dict(tag=0, cnt=0) for _ in range(NA * ACC)] for _ in range(grid)]
+    stored = [0] * count
+    got = [0] * count
+    res = dict(faults=0, newer=0)
+
+    def wait(cond):
+        polls = 0
+        while not cond():
+            polls += 1
+            if polls >= deadline:
+                res["faults"] += 1
+                return False
+            yield
+        return True
+
+    def fetch(L, b):
+        home = b % QSUB
+        d = L.drained
+        while d < QSUB:
+            k = home if d == 0 else (home + 1 + (d - 1 + (b // QSUB) % (QSUB - 1)) % (QSUB - 1)) % QSUB
+            t = bank.sub[k]
+            bank.sub[k] += 1
+            yield
+            if k + t * QSUB < nch:
+                return k + t * QSUB
+            L.drained = max(L.drained, d + 1)
+            yield
+            d = max(L.drained, d + 1)
+        return NOCH
+
+    def publish(L, seq, cid):
+        r = seq % RING
+        if seq >= RING:
+            yield from wait(lambda: L.reads[r] == cu)
+        L.reads[r] = 0
+        yield
+        L.entry[r] = (seq, cid)
+        yield
+
+    def take(L, b):  # UnitTaker::take_unit: (unit, seq) or None
+        while True:
+            t = L.slot
+            L.slot += 1
+            yield
+            seq, r = t >> cl, (t >> cl) % RING
+            if not (yield from wait(lambda: L.entry[r][0] == seq)):
+                return None
+            e = L.entry[r]
+            L.reads[r] += 1  # counted at once: no deferred reader
+            yield
+            if (t & (cu - 1)) == cu - lead:
+                nid = NOCH if e[1] == NOCH else (yield from fetch(L, b))
+                yield from publish(L, seq + 1, nid)
+            if e[1] == NOCH:
+                return None
+            k = t & (cu - 1)
+            if k < size(e[1]):
+                return start(e[1]) + k, seq
+
+    def accumulate(b, u, seq):
+        p = u >> psl
+        ent = acc[b][(seq % NA) * ACC + (p % ACC)]
+        me = seq + 1
+        while True:
+            tg = ent["tag"]
+            if tg == me:
+                break
+            if tg == 0:  # CAS 0 -> me
+                ent["tag"] = me
+                yield
+                break
+            if tg > me:
+                res["newer"] += 1
+                return
+            if not (yield from wait(lambda: ent["tag"] in (0, me))):
+                return
+        got[p] += 1
+        ent["cnt"] += 1
+        yield
+        if ent["cnt"] == pieces:
+            stored[p] += 1
+            ent["cnt"] = 0
+            yield
+            ent["tag"] = 0
+            yield
+
+    def wave(b, w):
+        L = lds[b]
+        while not L.ready:
+            yield
+        cur = yield from take(L, b)
+        while cur is not None:
+            for _ in range(rnd.randint(0, 60)):  # the piece's step loop
+                yield
+            nxt = yield from take(L, b)  # the next piece's loads go out here
+            for _ in range(rnd.randint(0, 6)):  # combine + shift
+                yield
+            yield from accumulate(b, *cur)
+            cur = nxt
+
+    def init(b):
+        L = lds[b]
+        yield from publish(L, 0, (yield from fetch(L, b)))
+        yield
+        L.ready = True
+
+    gens = [init(b) for b in range(grid)] + [wave(b, w) for b in range(grid) for w in range(wpw)]
+    steps = 0
+    while gens:
+        g = rnd.choice(gens)
+        try:
+            next(g)
+        except StopIteration:
+            gens.remove(g)
+        steps += 1
+        assert steps < max_steps, "no progress"
+    return stored, got, res
+
+
+@pytest.mark.parametrize("count,psl,grid,wpw", [(64, 2, 2, 4), (200, 2, 3, 8), (8192 // 16, 2, 4, 16),
+                                                (300, 1, 4, 4), (128, 2, 1, 16), (40, 2, 1, 4)])
+def test_split_pipelined_pieces_combine_exactly_once(count, psl, grid, wpw):
+    for seed in range(3):
+        stored, got, res = _split_model(count, psl, grid, wpw, seed * 131 + count)
+        assert res == dict(faults=0, newer=0), res
+        assert got == [1 << psl] * count, "a payload missed or doubled a piece"
+        assert stored == [1] * count, "a payload's CRC not stored exactly once"
