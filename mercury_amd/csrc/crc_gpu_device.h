@@ -207,7 +207,8 @@ constexpr uint32_t kWgChunkMaxLog2 = 5;
 // (non-temporal, >= 512 MiB) aligned CRC-32C batches, +2.3% on the headline.
 // Smaller fixed batches and CRC-64 fixed batches keep the static stride:
 // there the queue's fixed costs outweigh the balance (C2 -11% warm, -14%
-// with cold lines, profiles/r06/ab_c2cold.log; C3 -5%).
+// with cold lines, profiles/r06/ab_c2cold.log; 2 KiB -16% and 8/16 KiB
+// +-0.3% at the round-6 lane counts, profiles/r06/ab_c2dyn.log; C3 -5%).
 __host__ __device__ constexpr bool dyn_policy(int width, int mode, bool nt, bool light) {
     return !light && (mode == 2 || (width == 32 && nt && mode == 0));  // 2 = kOffsets
 }
