@@ -2,7 +2,9 @@
 """Per-wave timeline of one batch launch from a -DMCK_TRACE=1 build
 (make variants VARIANTS="trace:-DMCK_TRACE=1"): when waves enter, finish the
 LDS fill and exit, relative to the first entry (wall_clock64, 100 MHz).
-Shows the launch ramp and the tail that static payload assignment leaves."""
+Shows the launch ramp and the tail that static payload assignment leaves.
+ROTATE=R: R copies of each fixed batch, read in turn (cold lines, as
+bench.py --rotate), back-to-back launches with the traced one last."""
 import ctypes, json, os, sys
 import numpy as np
 import torch
@@ -31,6 +33,8 @@ def main():
             data = torch.empty(count * length + 64, dtype=torch.uint8, device="cuda")
             offs = None
         G.fill_splitmix(data, seed)
+        rot = int(os.environ.get("ROTATE", "1")) if offs is None else 1
+        copies = [data] + [data.clone() for _ in range(rot - 1)]
         o = torch.empty(count, dtype=torch.int32 if method == "crc32c" else torch.int64, device="cuda")
         s = torch.cuda.current_stream().cuda_stream
         assert lib.mchecksum_gpu_prepare(method.encode()) == 0
@@ -39,8 +43,12 @@ def main():
             buf = np.zeros(3 * 16384, dtype=np.uint64)
             lib.mck_debug_trace_read(buf.ctypes.data, buf.nbytes)  # (stale values are masked below)
             torch.cuda.synchronize()
+            for b in range(rot - 1):  # the launches before the traced one, back to back
+                assert lib.mchecksum_gpu_checksum_fixed(method.encode(), copies[b].data_ptr(), length, length, count,
+                                                        o.data_ptr(), s) == 0
             if offs is None:
-                rc = lib.mchecksum_gpu_checksum_fixed(method.encode(), data.data_ptr(), length, length, count, o.data_ptr(), s)
+                rc = lib.mchecksum_gpu_checksum_fixed(method.encode(), copies[-1].data_ptr(), length, length, count,
+                                                      o.data_ptr(), s)
             else:
                 rc = lib.mchecksum_gpu_checksum_offsets(method.encode(), data.data_ptr(), offs.data_ptr(), count, o.data_ptr(), s)
             assert rc == 0
@@ -79,7 +87,7 @@ def main():
         med["end_mean_per_xcd_us(last)"] = res[-1]["end_mean_per_xcd_us"]
         print(cfg, json.dumps(med), flush=True)
         out[cfg] = med
-        del data
+        del data, copies
         torch.cuda.empty_cache()
     json.dump(out, open(os.path.join(ROOT, "gpurun_out", os.environ.get("TRACE_OUT", "tail_trace.json")), "w"), indent=1)
 
