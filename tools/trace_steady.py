@@ -5,7 +5,14 @@ DESIGN.md sec. 6) and the last `steps` ones (the timed region).  The mean over
 the timed dispatches is the rocprof counterpart of bench.py's
 roofline.kernel_ms; the --stats summary averages over every dispatch.
 
-usage: trace_steady.py KERNEL_TRACE.csv KERNEL_SUBSTRING WARMUP STEPS [BENCH.json] > out.json
+usage: trace_steady.py KERNEL_TRACE.csv KERNEL_SUBSTRING WARMUP STEPS [BENCH.json] [--skip N] > out.json
+
+By default the timed region is the kernel's last STEPS dispatches.  With
+--skip N it is dispatches [N + WARMUP, N + WARMUP + STEPS) in time order: the
+default bench.py line launches the headline's kernel first for c5_strong and
+then for the e2e zero-copy leg, and the headline's own dispatches come last
+(the default region); c5_strong's region is --skip 0, and BENCH.json's
+c5_strong.kernel_ms is its counterpart.
 """
 import csv
 import json
@@ -14,27 +21,39 @@ import sys
 
 
 def main():
-    path, key, warmup, steps = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4])
+    argv = sys.argv[1:]
+    skip = None
+    if "--skip" in argv:
+        i = argv.index("--skip")
+        skip = int(argv[i + 1])
+        del argv[i:i + 2]
+    path, key, warmup, steps = argv[0], argv[1], int(argv[2]), int(argv[3])
     rows = [r for r in csv.DictReader(open(path)) if key in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     us = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows]
-    if len(us) < warmup + steps:
-        raise SystemExit(f"{len(us)} dispatches of {key!r}, expected >= {warmup + steps}")
-    timed = us[-steps:]
+    need = warmup + steps + (skip or 0)
+    if len(us) < need:
+        raise SystemExit(f"{len(us)} dispatches of {key!r}, expected >= {need}")
+    if skip is None:
+        warm, timed = us[len(us) - steps - warmup:len(us) - steps], us[-steps:]
+    else:
+        warm, timed = us[skip:skip + warmup], us[skip + warmup:skip + warmup + steps]
     out = {
         "kernel": rows[0]["Kernel_Name"],
         "dispatches": len(us),
         "all_mean_us": round(statistics.mean(us), 2),
-        "warmup_mean_us": round(statistics.mean(us[:warmup]), 2) if warmup else None,
+        "region": "last" if skip is None else f"skip {skip}",
+        "warmup_mean_us": round(statistics.mean(warm), 2) if warmup else None,
         "timed_mean_us": round(statistics.mean(timed), 2),
         "timed_median_us": round(statistics.median(timed), 2),
         "timed_min_us": round(min(timed), 2),
         "timed_max_us": round(max(timed), 2),
     }
-    if len(sys.argv) > 5:
-        b = json.load(open(sys.argv[5]))
-        out["bench_kernel_ms"] = b["roofline"]["kernel_ms"]
-        out["timed_mean_vs_bench"] = round(out["timed_mean_us"] / 1e3 / b["roofline"]["kernel_ms"], 4)
+    if len(argv) > 4:
+        b = json.load(open(argv[4]))
+        out["bench_kernel_ms"] = (b["c5_strong"]["kernel_ms"] if skip is not None and "c5_strong" in b
+                                  else b["roofline"]["kernel_ms"])
+        out["timed_mean_vs_bench"] = round(out["timed_mean_us"] / 1e3 / out["bench_kernel_ms"], 4)
     json.dump(out, sys.stdout, indent=1)
     print()
 
