@@ -104,17 +104,22 @@ settings_from_env(void)
 static const mck_settings_t *_Atomic g_settings;
 static pthread_once_t g_settings_once = PTHREAD_ONCE_INIT;
 static pthread_mutex_t g_settings_mu = PTHREAD_MUTEX_INITIALIZER;
-static const mck_settings_t g_settings_fallback = {.crc64_idx = 2, .crc16_idx = 11, .gpu_log2g = -1,
-                                                   .gpu_light = -1, .gpu_nt = -1, .gpu_split = -1,
-                                                   .gpu_split_lds = 1, .gpu_xdr_fast = -1,
-                                                   .gpu_seg_map_cap = UINT64_MAX, .qfault_scan = UINT64_MAX};
+/* the defaults, if the first snapshot cannot be allocated */
+static mck_settings_t g_settings_fallback = {.gpu_log2g = -1, .gpu_light = -1, .gpu_nt = -1, .gpu_split = -1,
+                                             .gpu_split_lds = 1, .gpu_xdr_fast = -1,
+                                             .gpu_seg_map_cap = UINT64_MAX, .qfault_scan = UINT64_MAX};
 
 static void
 settings_init(void)
 {
     const mck_settings_t *s = settings_from_env();
 
-    __atomic_store_n(&g_settings, s ? s : &g_settings_fallback, __ATOMIC_RELEASE);
+    if (!s) {
+        g_settings_fallback.crc64_idx = find(MCK_DEFAULT_CRC64);
+        g_settings_fallback.crc16_idx = find(MCK_DEFAULT_CRC16);
+        s = &g_settings_fallback;
+    }
+    __atomic_store_n(&g_settings, s, __ATOMIC_RELEASE);
 }
 
 const mck_settings_t *
