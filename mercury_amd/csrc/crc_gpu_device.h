@@ -1821,8 +1821,10 @@ __global__ __launch_bounds__(kBlk64<MODE * 16 + LOG2G>, kWpe64<MODE * 16 + LOG2G
         // its ring entry: set seq % kAccSets, owner tag seq + 1.  A piece
         // whose entry an older chunk still holds waits for it (bounded; the
         // older chunk's pieces are all taken and never wait on this one); a
-        // newer owner means the pieces in flight spanned kAccSets chunks,
-        // impossible with <= 32 pieces in flight -- a fault, never a value.
+        // newer owner means one wave held every taken piece of its chunk while
+        // the workgroup's other waves finished kAccSets - 1 whole chunks (most
+        // of a launch at a 256 KiB piece per wave and chunk) -- a fault, never
+        // a value.
         const uint32_t pieces = 1u << splan.psl;
         const uint64_t bytes = a.len >> splan.psl;  // kSplitBytes
         const uint32_t K = (uint32_t)(bytes >> 10);
