@@ -196,19 +196,22 @@ def main():
     if args.backend == "nccl" and len(set(keys)) != world:
         sys.exit(f"bench.py: ranks share a GPU ({pcis}): one GPU per rank")
 
+    # The sub-records run before the headline, so the headline's dispatches
+    # are the last of their kernel in a profile of this command, in the order
+    # e2e, c5_strong, headline: with the PCIe-bound e2e second between
+    # c5_strong and the headline, the headline measured ~1% lower and noisier
+    # (0.837-0.856 vs 0.854-0.857 on one box, profiles/r06/order/).
+    e2e = None
+    if args.config == "metric" and not args.no_e2e and world == 1:
+        # north_star's end-to-end rate: the headline's bytes starting and
+        # ending in host memory (NA recv buffers / hg_proc buffers)
+        e2e = run_e2e(args, torch, dev)
     c5_strong = None
     if args.config == "metric" and not args.no_c5_strong:
         # BASELINE configs[4] in the same run, whatever flags the driver
         # passes: C5's fixed 2^20 x 64 KiB batch split over the ranks (strong
-        # scaling).  Measured first, so the headline's dispatches are the last
-        # of their kernel in a profile of this command.
+        # scaling)
         c5_strong = run_c5_strong(args, torch, dist, dist_on, rank, world, dev, coll_dev)
-    e2e = None
-    if args.config == "metric" and not args.no_e2e and world == 1:
-        # north_star's end-to-end rate: the headline's bytes starting and
-        # ending in host memory (NA recv buffers / hg_proc buffers).  Before
-        # the headline, so its dispatches stay the last of their kernel.
-        e2e = run_e2e(args, torch, dev)
 
     from mercury_amd import gpu as G
     from mercury_amd.shard import batch_shard

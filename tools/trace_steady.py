@@ -9,9 +9,10 @@ usage: trace_steady.py KERNEL_TRACE.csv KERNEL_SUBSTRING WARMUP STEPS [BENCH.jso
 
 By default the timed region is the kernel's last STEPS dispatches.  With
 --skip N it is dispatches [N + WARMUP, N + WARMUP + STEPS) in time order: the
-default bench.py line launches the headline's kernel first for c5_strong and
-then for the e2e zero-copy leg, and the headline's own dispatches come last
-(the default region); c5_strong's region is --skip 0, and BENCH.json's
+default bench.py line launches the headline's kernel first for the e2e
+zero-copy leg (1 + --e2e-reps launches), then for c5_strong, and the
+headline's own dispatches come last (the default region); c5_strong's region
+is --skip 6 at the default 5 reps (--skip 0 with --no-e2e), and BENCH.json's
 c5_strong.kernel_ms is its counterpart.
 """
 import csv
