@@ -1193,8 +1193,25 @@ __device__ __forceinline__ unsigned int xcc_id() {
 #define MCK_STAMP(w, k) do { } while (0)
 #endif
 
+// A verify launch counts its mismatches per lane (nbad) and adds them to the
+// caller's counter once per WORKGROUP at its end.  Device-scope atomics on one
+// word serialize: one per bad payload (or per wave) made 4096 bad 4 KiB
+// messages a 58 us kernel against 19 us when they all matched
+// (tools/lat_offsets.py), so a corrupted buffer cost three times a good one.
+// Every thread of the workgroup calls this, once.
+__device__ __forceinline__ void add_mismatches(uint32_t *ctr, uint32_t nbad) {
+    __shared__ uint32_t wg_bad;
+    if (threadIdx.x == 0) wg_bad = 0;
+    __syncthreads();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) nbad += __shfl_xor(nbad, d, 64);
+    if ((threadIdx.x & 63u) == 0 && nbad) atomicAdd(&wg_bad, nbad);
+    __syncthreads();
+    if (threadIdx.x == 0 && wg_bad && ctr) atomicAdd(ctr, wg_bad);
+}
+
 template <typename T, bool VERIFY>
-__device__ __forceinline__ void emit(const BatchArgs &a, uint64_t p, T v) {
+__device__ __forceinline__ void emit(const BatchArgs &a, uint64_t p, T v, uint32_t &nbad) {
     if (VERIFY) {
         if (a.bswap) {
             if constexpr (sizeof(T) == 8) v = (T)__builtin_bswap64((uint64_t)v);
@@ -1202,7 +1219,7 @@ __device__ __forceinline__ void emit(const BatchArgs &a, uint64_t p, T v) {
         }
         const bool bad = reinterpret_cast<const T *>(a.expected)[p] != v;
         if (a.status) a.status[p] = bad ? 1 : 0;
-        if (bad && a.mismatches) atomicAdd(a.mismatches, 1u);
+        nbad += bad;
     } else {
         reinterpret_cast<T *>(a.out)[p] = v;
     }
@@ -1256,6 +1273,7 @@ __global__ __launch_bounds__(kBlk32<LIGHT>, 1) void crc32c_batch_kernel(BatchArg
     const Tab32<LIGHT> lds{lds_raw};
 
     const uint32_t lc0 = (lane & 31u) << 2, lc1 = lc0 | 0x10000u;
+    uint32_t nbad = 0;  // verify: this lane's mismatches (add_mismatches)
 
     if (MODE == kOffsets) {
         auto one = [&](uint64_t p) {
@@ -1270,9 +1288,9 @@ __global__ __launch_bounds__(kBlk32<LIGHT>, 1) void crc32c_batch_kernel(BatchArg
                 if (VERIFY && a.msg) {
                     const bool bad = short_msg || load_be32(a.base + m0 + a.hash_off) != (x ^ xorout);
                     if (a.status) a.status[p] = bad ? 1 : 0;
-                    if (bad && a.mismatches) atomicAdd(a.mismatches, 1u);
+                    nbad += bad;
                 } else {
-                    emit<uint32_t, VERIFY>(a, p, x ^ xorout);
+                    emit<uint32_t, VERIFY>(a, p, x ^ xorout, nbad);
                 }
             }
         };
@@ -1283,6 +1301,7 @@ __global__ __launch_bounds__(kBlk32<LIGHT>, 1) void crc32c_batch_kernel(BatchArg
             wave_range(a.offsets, a.count, wave, nw, &first, &last);
             for (uint64_t p = first; p < last; p++) one(p);
         }
+        if constexpr (VERIFY) add_mismatches(a.mismatches, nbad);
         MCK_STAMP(wave, 2);
         return;
     }
@@ -1296,7 +1315,7 @@ __global__ __launch_bounds__(kBlk32<LIGHT>, 1) void crc32c_batch_kernel(BatchArg
                                              loaded);
         else
             x = payload32_generic<LOG2G, NT>(lds, pk, a.base + pc * a.stride, a.len, gl, lc0, lc1);
-        if (act && gl == 0) emit<uint32_t, VERIFY>(a, p, x ^ xorout);
+        if (act && gl == 0) emit<uint32_t, VERIFY>(a, p, x ^ xorout, nbad);
     };
     // The prefetched first unit runs in a copy of the payload loop of its own:
     // one copy behind a loaded/not-loaded branch leaves the prefetch loads
@@ -1305,6 +1324,7 @@ __global__ __launch_bounds__(kBlk32<LIGHT>, 1) void crc32c_batch_kernel(BatchArg
     if (PRE && pre) unit(wave, true);
     const bool faulted = for_each_unit<DYN, PRE>(&wgq, a.queue, units, wave, nw, [&](uint64_t u) { unit(u, false); });
     if (faulted) fail_closed<VERIFY>(a);
+    if constexpr (VERIFY) add_mismatches(a.mismatches, nbad);
     MCK_STAMP(wave, 2);
 }
 
@@ -1773,6 +1793,7 @@ __global__ __launch_bounds__(kBlk64<MODE * 16 + LOG2G>, kWpe64<MODE * 16 + LOG2G
     const uint32_t lc = (lane & 31u) << 3;
     const uint64_t xorout = pk->xorout;
     const uint32_t nw = gridDim.x * kWPB;
+    uint32_t nbad = 0;  // verify: this lane's mismatches (add_mismatches)
     // A static split with fewer units than waves numbers the waves across
     // workgroups first, so a small batch spreads over CUs (the host then
     // launches one workgroup per unit) instead of filling one CU's LDS
@@ -1787,9 +1808,10 @@ __global__ __launch_bounds__(kBlk64<MODE * 16 + LOG2G>, kWpe64<MODE * 16 + LOG2G
             const uint64_t n = a.offsets[p + 1] - o;
             const uint64_t x = n < (1ull << 31) ? payload64_g64<NT, false, S::ops_mode>(lds, pk, a.base + o, n, gl, lc)
                                                 : payload64_generic<LOG2G, NT, S::ops_mode>(lds, pk, a.base + o, n, gl, lc);
-            if (gl == 0) emit<uint64_t, VERIFY>(a, p, x ^ xorout);
+            if (gl == 0) emit<uint64_t, VERIFY>(a, p, x ^ xorout, nbad);
         };
         if (for_each_unit<true>(&wgq, a.queue, units, wave, nw, one)) fail_closed<VERIFY>(a);
+        if constexpr (VERIFY) add_mismatches(a.mismatches, nbad);
         return;
     }
     if constexpr (SPLIT) {
@@ -1923,9 +1945,10 @@ __global__ __launch_bounds__(kBlk64<MODE * 16 + LOG2G>, kWpe64<MODE * 16 + LOG2G
             x = payload64_aligned<LOG2G, NT, S::ops_mode>(lds, pk, a.base + pc * a.stride, (uint32_t)(a.len >> (4 + LOG2G)), gl, lc, pk->init);
         else
             x = payload64_generic<LOG2G, NT>(lds, pk, a.base + pc * a.stride, a.len, gl, lc);
-        if (act && gl == 0) emit<uint64_t, VERIFY>(a, p, x ^ xorout);
+        if (act && gl == 0) emit<uint64_t, VERIFY>(a, p, x ^ xorout, nbad);
     });
     if (faulted) fail_closed<VERIFY>(a);
+    if constexpr (VERIFY) add_mismatches(a.mismatches, nbad);
     MCK_STAMP(blockIdx.x * kWPB + (threadIdx.x >> 6), 2);
 }
 

@@ -718,6 +718,7 @@ __global__ __launch_bounds__(256) void core_header_kernel(HdrArgs a) {
     __shared__ uint16_t T[256];
     T[threadIdx.x] = a.table[threadIdx.x];
     __syncthreads();
+    uint32_t nbad = 0;
     for (uint64_t m = (uint64_t)blockIdx.x * 256 + threadIdx.x; m < a.count; m += (uint64_t)gridDim.x * 256) {
         const uint64_t o = a.off[m];
         const bool whole = a.off[m + 1] - o >= kHdrSize;
@@ -751,8 +752,9 @@ __global__ __launch_bounds__(256) void core_header_kernel(HdrArgs a) {
         }
         const bool bad = !whole || ((r ^ a.xorout) & 0xFFFFu) != wire;
         if (a.status) a.status[m] = bad ? 1 : 0;
-        if (bad && a.mism) atomicAdd(a.mism, 1u);
+        nbad += bad;
     }
+    add_mismatches(a.mism, nbad);  // once per workgroup (crc_gpu_device.h)
 }
 
 // ------------------------------------------------------------------ XDR ----
