@@ -1484,6 +1484,28 @@ __device__ __forceinline__ uint64_t combine64(const uint8_t *lds, const crc64_gp
     return x;
 }
 
+// The same sum as a halving reduction (lane 0 of each group of G lanes): at
+// distance d = G/2, ..., 2, 1 the lanes below d add Z^-(16d) of the state d
+// lanes up, so level d's lookups run on d lanes where the butterfly's ran on
+// all G, and lane 0 ends with the sum (payload64_g64 then runs its tail
+// operators on lane 0 alone).  C4-layout CRC-64 +3.1% / +2.4%
+// (profiles/r06/ab_c4_64_combine.log, ab_lane0.log: the combine and tail were
+// 14% of that kernel's time; running the tail on the wave-uniform value
+// through the scalar cache instead cost 9%).  The C3 split pieces and the
+// segment chunk pass measured +-0 / -0.9% with it and keep the butterfly.
+template <int LOG2G, int OM>
+__device__ __forceinline__ uint64_t combine64_lane0(const uint8_t *lds, const crc64_gpu_pack_t *pk, uint64_t s0,
+                                                    uint64_t s1, uint32_t gl) {
+    uint64_t x = s0 ^ opm64<OM>(lds, pk, 0, s1);
+#pragma unroll
+    for (int k = LOG2G - 1; k >= 0; k--) {
+        const uint32_t d = 1u << k;
+        const uint64_t hi = __shfl_down(x, d, 64);
+        if (gl < d) x ^= opm64<OM>(lds, pk, 1 + k, hi);
+    }
+    return x;
+}
+
 template <int BLOCK, int OM>
 __device__ void fill_lds64(uint8_t *lds, const crc64_gpu_pack_t *pk) {
     uint64_t *l = reinterpret_cast<uint64_t *>(lds);
@@ -1743,8 +1765,9 @@ __device__ __forceinline__ uint64_t payload64_g64(const uint8_t *lds, const crc6
             if (k + u < K) fold(k + u, v);
         }
     }
-    uint64_t x = combine64<6, OM>(lds, pk, x0, x1, gl);
-    x = tail64<OM>(lds, pk, (uint32_t)(a1 - ea), x);
+    uint64_t x = combine64_lane0<6, OM>(lds, pk, x0, x1, gl);
+    if (gl == 0) x = tail64<OM>(lds, pk, (uint32_t)(a1 - ea), x);
+    x = uniform64(x);
     if (!RAW && len < 8) x ^= pk->zinit[len];
     return x;
 }
