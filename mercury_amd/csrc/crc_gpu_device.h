@@ -1492,7 +1492,8 @@ __device__ __forceinline__ uint64_t combine64(const uint8_t *lds, const crc64_gp
 // (profiles/r06/ab_c4_64_combine.log, ab_lane0.log: the combine and tail were
 // 14% of that kernel's time; running the tail on the wave-uniform value
 // through the scalar cache instead cost 9%).  The C3 split pieces and the
-// segment chunk pass measured +-0 / -0.9% with it and keep the butterfly.
+// segment chunk pass measured +-0 / -0.9% with it and keep the butterfly;
+// payload64_g64 uses it only in the offsets kernels (kOpsMix).
 template <int LOG2G, int OM>
 __device__ __forceinline__ uint64_t combine64_lane0(const uint8_t *lds, const crc64_gpu_pack_t *pk, uint64_t s0,
                                                     uint64_t s1, uint32_t gl) {
@@ -1765,9 +1766,17 @@ __device__ __forceinline__ uint64_t payload64_g64(const uint8_t *lds, const crc6
             if (k + u < K) fold(k + u, v);
         }
     }
-    uint64_t x = combine64_lane0<6, OM>(lds, pk, x0, x1, gl);
-    if (gl == 0) x = tail64<OM>(lds, pk, (uint32_t)(a1 - ea), x);
-    x = uniform64(x);
+    uint64_t x;
+    if constexpr (OM == kOpsMix) {  // the offsets batches (see combine64_lane0)
+        x = combine64_lane0<6, OM>(lds, pk, x0, x1, gl);
+        if (gl == 0) x = tail64<OM>(lds, pk, (uint32_t)(a1 - ea), x);
+        x = uniform64(x);
+    } else {  // the segment and XDR kernels: the halving form there cost the
+              // segment chunk pass 6.8% (register allocation of its other paths,
+              // profiles/r06/ab_seg_lane0.log)
+        x = combine64<6, OM>(lds, pk, x0, x1, gl);
+        x = tail64<OM>(lds, pk, (uint32_t)(a1 - ea), x);
+    }
     if (!RAW && len < 8) x ^= pk->zinit[len];
     return x;
 }
